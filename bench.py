@@ -1,0 +1,246 @@
+#!/usr/bin/env python3
+"""Benchmark: device-resident MPI_Reduce_local, fp32 MPI_SUM, 256 MiB per operand per GPU.
+
+BASELINE.json metric "GiB/s device-resident MPI_Reduce_local (fp32 SUM,
+256 MiB) at 1/2/4/8 GPUs".  One process per GPU (torchrun for N > 1); every
+rank combines its own resident (inbuf, inoutbuf) pair -- MPI_Reduce_local is
+element-wise and has no exchange step, so ranks shard with no collective on
+the data path ("scaling": "weak").  torch.distributed is used only for the
+barrier and the max-over-ranks of the elapsed time.
+
+A step is one MPI_Reduce_local(inbuf, inoutbuf, 67108864, MPI_FLOAT, MPI_SUM)
+call through the C ABI -- the public, synchronous entry point (it returns
+with the result complete).  Timed: exactly K steps between barrier +
+torch.cuda.synchronize() on both sides, after W untimed warm-up steps.
+    value = 3 * 256 MiB * K * N / max_rank_seconds / 2^30   (GiB/s, algorithmic bytes:
+            read inbuf, read inoutbuf, write inoutbuf -- SURVEY.md §8d)
+
+Extra fields (rank 0):
+  roofline      dominant kernel (k_reduce_tile<OpSum,float>): algorithmic bytes per
+                launch / mean launch duration from HIP events recorded on the
+                stream the kernel runs on (MPIX_Reduce_local_stream onto a torch
+                stream), vs the 8.0 TB/s HBM3E peak; traffic = per-launch HBM
+                bytes from the committed rocprofv3 PMC summary (profiles/) if present.
+  stream_api    the same combine enqueued back-to-back with MPIX_Reduce_local_stream
+                (the async variant the library's own schedules use).
+  pcie_inclusive  pinned host buffers -> MPI_Reduce_local (H2D + kernel + D2H),
+                the rate when rank buffers arrive in host memory over PiP shm.
+                Reported for DESIGN.md; never `value`.
+  cpu_baseline  the oracle's C loop (reference algorithm, gcc -O2) timed on this
+                box's host cores on a bounded sample (rank 0, N = 1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "mpich-pip_amd"))
+sys.path.insert(0, ROOT)
+
+MIB = 1 << 20
+GIB = 1 << 30
+HBM_PEAK_BPS = 8.0e12          # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+METRIC = "GiB/s device-resident MPI_Reduce_local (fp32 SUM, 256 MiB) at 1/2/4/8 GPUs"
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--mib", type=int, default=256, help="MiB per operand (metric: 256)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-extras", action="store_true", help="only the timed MPI_Reduce_local loop")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="cpu_baseline threads (0 = min(16, affinity))")
+    ap.add_argument("--cpu-iters", type=int, default=8)
+    return ap.parse_args()
+
+
+def time_steps(step, k: int, w: int, sync, barrier, max_over_ranks) -> float:
+    """W untimed steps, then exactly K steps bracketed by barrier + device sync; max over ranks."""
+    for i in range(w):
+        step(i)
+    sync()
+    barrier()
+    sync()
+    t0 = time.perf_counter()
+    for i in range(k):
+        step(w + i)
+    sync()
+    t1 = time.perf_counter()
+    barrier()
+    return max_over_ranks(t1 - t0)
+
+
+def load_traffic(count_bytes: int):
+    """Per-launch HBM bytes of the dominant kernel from the committed PMC summary."""
+    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        d = json.load(open(p))
+    except (OSError, ValueError):
+        return None, None
+    if d.get("operand_bytes") != count_bytes:
+        return None, None
+    return d.get("hbm_bytes_per_launch"), os.path.relpath(p, ROOT)
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+    import mpich_pip_amd as m
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE", file=sys.stderr)
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    def max_over_ranks(x: float) -> float:
+        if world == 1:
+            return x
+        t = torch.tensor([x], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    sync = torch.cuda.synchronize
+    lib = m.load()
+    lib.MPIX_Reduce_local_set_errhandler(m.MPI_ERRORS_RETURN)
+
+    nbytes = args.mib * MIB
+    count = nbytes // 4
+    alg_bytes = 3 * nbytes
+    g = torch.Generator(device="cuda").manual_seed(0x5EED + rank)
+    # two resident pairs, alternated, so consecutive steps never hit the
+    # Infinity Cache lines the previous step left behind
+    pairs = [((torch.rand(count, device="cuda", generator=g) * 2 - 1),
+              (torch.rand(count, device="cuda", generator=g) * 2 - 1)) for _ in range(2)]
+    ptrs = [(a.data_ptr(), b.data_ptr()) for a, b in pairs]
+    sync()
+
+    def step(i):
+        pin, pio = ptrs[i & 1]
+        rc = lib.MPI_Reduce_local(pin, pio, count, m.MPI_FLOAT, m.MPI_SUM)
+        if rc:
+            raise RuntimeError(m.error_string(rc))
+
+    dt = time_steps(step, args.steps, args.warmup, sync, barrier, max_over_ranks)
+    value = alg_bytes * args.steps * world / dt / GIB
+
+    out = {
+        "metric": METRIC,
+        "value": round(value, 1),
+        "unit": "GiB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(dt / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (uniform [-1,1) fp32, seed 0x5EED+rank), device-resident",
+        "config": {
+            "workload": "MPI_Reduce_local MPI_SUM MPI_FLOAT, %d MiB per operand per GPU (count %d), "
+                        "device-resident, one rank per GPU" % (args.mib, count),
+            "count": count,
+            "algorithmic_bytes_per_call": alg_bytes,
+            "api": "MPI_Reduce_local (C ABI, synchronous)",
+            "parallelism": "replica-per-gpu (no data-path collective)",
+        },
+    }
+
+    if not args.no_extras:
+        # ---- roofline: per-launch kernel time with HIP events on the kernel's stream
+        s = torch.cuda.Stream()
+        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+               for _ in range(args.steps)]
+        with torch.cuda.stream(s):
+            for i in range(args.warmup):
+                pin, pio = ptrs[i & 1]
+                lib.MPIX_Reduce_local_stream(pin, pio, count, m.MPI_FLOAT, m.MPI_SUM, s.cuda_stream)
+            for i, (e0, e1) in enumerate(evs):
+                pin, pio = ptrs[i & 1]
+                e0.record(s)
+                rc = lib.MPIX_Reduce_local_stream(pin, pio, count, m.MPI_FLOAT, m.MPI_SUM, s.cuda_stream)
+                e1.record(s)
+                assert rc == 0
+        s.synchronize()
+        ms = sorted(e0.elapsed_time(e1) for e0, e1 in evs)
+        mean_ms = sum(ms) / len(ms)
+        achieved = alg_bytes / (mean_ms * 1e-3)
+        traffic, tsrc = load_traffic(nbytes)
+        out["roofline"] = {
+            "bound": "hbm",
+            "kernel": "mpir_hip::k_reduce_tile<OpSum,float>",
+            "achieved": round(achieved / 1e9, 1),
+            "peak": HBM_PEAK_BPS / 1e9,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_BPS, 4),
+            "traffic": traffic,
+            "traffic_source": tsrc,
+            "algorithmic_bytes_per_launch": alg_bytes,
+            "mean_launch_us": round(mean_ms * 1e3, 2),
+            "median_launch_us": round(ms[len(ms) // 2] * 1e3, 2),
+            "p10_p90_us": [round(ms[len(ms) // 10] * 1e3, 2), round(ms[(len(ms) * 9) // 10] * 1e3, 2)],
+        }
+
+        # ---- stream-ordered API, back to back (what the library's schedules drive)
+        def sstep(i):
+            pin, pio = ptrs[i & 1]
+            lib.MPIX_Reduce_local_stream(pin, pio, count, m.MPI_FLOAT, m.MPI_SUM, None)
+        dts = time_steps(sstep, args.steps, args.warmup, sync, barrier, max_over_ranks)
+        out["stream_api"] = {"value": round(alg_bytes * args.steps * world / dts / GIB, 1), "unit": "GiB/s",
+                             "ms_per_step": round(dts / args.steps * 1e3, 4),
+                             "api": "MPIX_Reduce_local_stream, synchronised once per K steps"}
+
+        # ---- PCIe-inclusive: rank buffers in pinned host memory (PiP shm)
+        ha = pairs[0][0].cpu().pin_memory()
+        hb = pairs[0][1].cpu().pin_memory()
+        hk = max(3, min(10, args.steps))
+
+        def hstep(i):
+            rc = lib.MPI_Reduce_local(hb.data_ptr(), ha.data_ptr(), count, m.MPI_FLOAT, m.MPI_SUM)
+            assert rc == 0
+        dth = time_steps(hstep, hk, 1, sync, barrier, max_over_ranks)
+        out["pcie_inclusive"] = {"value": round(alg_bytes * hk * world / dth / GIB, 2), "unit": "GiB/s",
+                                 "ms_per_step": round(dth / hk * 1e3, 3),
+                                 "note": "pinned host in/inout: H2D x2 + kernel + D2H per 64 MiB chunk"}
+        del ha, hb
+
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        import oracle
+        try:
+            aff = len(os.sched_getaffinity(0))
+        except AttributeError:
+            aff = os.cpu_count() or 1
+        threads = args.cpu_threads or max(1, min(16, aff))
+        secs = oracle.cpu_baseline_sum_f32(threads, count, args.cpu_iters)
+        if secs > 0:
+            cv = alg_bytes * args.cpu_iters * threads / secs / GIB
+            out["cpu_baseline"] = {
+                "value": round(cv, 2), "unit": "GiB/s", "cores": threads, "kind": "port",
+                "sample": f"{threads} threads x {args.cpu_iters} calls, each thread its own "
+                          f"{args.mib} MiB fp32 (inbuf, inoutbuf) pair; oracle/op_oracle.c SUM loop, gcc -O2",
+                "per_core": round(cv / threads, 2),
+                "seconds": round(secs, 3),
+            }
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,84 @@
+/*
+ * mpir_hip_reduce.h -- the thin C-ABI shim between MPICH's host C op layer
+ * and the gfx950 HIP kernels.  Plain pointers and sizes only.
+ *
+ * The host C layer (the C files under mpich-pip_amd/csrc/host) keeps the reference's
+ * structure: MPIR_SUM(invec, inoutvec, len, type) switches over the MPI
+ * datatype exactly like src/mpi/coll/op/opsum.c:21-76, and where the
+ * reference runs its scalar loop (MPIR_OP_TYPE_REDUCE_CASE,
+ * src/include/mpir_op_util.h:48-55) it calls MPIR_Hip_reduce() with the
+ * resolved (op, element class) pair instead.
+ */
+#ifndef MPIR_HIP_REDUCE_H_INCLUDED
+#define MPIR_HIP_REDUCE_H_INCLUDED
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* op codes == the reference's MPIR_Op_table index (allreduce.c:121-129) */
+enum MPIR_Hip_op {
+    MPIR_HIP_OP_MAX = 1,
+    MPIR_HIP_OP_MIN = 2,
+    MPIR_HIP_OP_SUM = 3,
+    MPIR_HIP_OP_PROD = 4,
+    MPIR_HIP_OP_LAND = 5,
+    MPIR_HIP_OP_BAND = 6,
+    MPIR_HIP_OP_LOR = 7,
+    MPIR_HIP_OP_BOR = 8,
+    MPIR_HIP_OP_LXOR = 9,
+    MPIR_HIP_OP_BXOR = 10,
+    MPIR_HIP_OP_MINLOC = 11,
+    MPIR_HIP_OP_MAXLOC = 12,
+    MPIR_HIP_OP_REPLACE = 13,
+    MPIR_HIP_NOPS = 14
+};
+
+/* element classes: the device storage type an MPI basic type maps to */
+enum MPIR_Hip_elem {
+    MPIR_HIP_I8 = 1, MPIR_HIP_U8, MPIR_HIP_I16, MPIR_HIP_U16,
+    MPIR_HIP_I32, MPIR_HIP_U32, MPIR_HIP_I64, MPIR_HIP_U64,
+    MPIR_HIP_F16, MPIR_HIP_F32, MPIR_HIP_F64,
+    MPIR_HIP_CF32, MPIR_HIP_CF64,                 /* C float/double _Complex */
+    MPIR_HIP_P2INT, MPIR_HIP_PFLOATINT, MPIR_HIP_PLONGINT,
+    MPIR_HIP_PSHORTINT, MPIR_HIP_PDOUBLEINT,      /* MAXLOC/MINLOC pairs */
+    MPIR_HIP_NELEMS
+};
+
+/* return codes */
+#define MPIR_HIP_OK        0
+#define MPIR_HIP_EBUFFER   1   /* host-only pointer where device memory is required */
+#define MPIR_HIP_ERUNTIME  2   /* HIP runtime failure; see MPIR_Hip_error_string() */
+#define MPIR_HIP_ENOKERNEL 3   /* (op, elem) pair has no kernel */
+#define MPIR_HIP_ENODEV    4   /* no usable GPU */
+
+/* Combine inoutbuf[i] = op(inoutbuf[i], inbuf[i]) for i < count elements of
+ * class `elem`.  Pointers may be device, pinned-host or pageable-host memory
+ * in any mix (host operands are staged through device scratch).
+ * hip_stream: a hipStream_t, or NULL for the calling thread's library stream
+ * on the device that owns inoutbuf.  sync != 0: wait for completion (and for
+ * the copy-back of a host inoutbuf) before returning.  sync == 0 requires
+ * both buffers device-resident on one device (else MPIR_HIP_EBUFFER). */
+int MPIR_Hip_reduce(const void *inbuf, void *inoutbuf, uint64_t count, int op, int elem,
+                    void *hip_stream, int sync);
+
+/* byte size of an element class (0 if unknown) */
+size_t MPIR_Hip_elem_size(int elem);
+/* 1 if a kernel exists for (op, elem) */
+int MPIR_Hip_has_kernel(int op, int elem);
+/* 1 if p is device-accessible memory (hipMalloc / managed), 0 otherwise */
+int MPIR_Hip_is_device_ptr(const void *p);
+/* synchronous copy between any two pointers (device/host in any mix) */
+int MPIR_Hip_memcpy(void *dst, const void *src, size_t bytes);
+/* last runtime error text for this thread ("" if none) */
+const char *MPIR_Hip_error_string(void);
+/* number of visible devices (0 if none / runtime unavailable) */
+int MPIR_Hip_device_count(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MPIR_HIP_REDUCE_H_INCLUDED */

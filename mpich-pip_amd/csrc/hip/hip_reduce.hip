@@ -1,0 +1,260 @@
+// hip_reduce.hip -- C-ABI shim: (op, element class) dispatch, pointer
+// classification, per-thread streams, host-operand staging.
+//
+// Replaces the scalar loop body the reference runs inside each MPIR_<OP>
+// (src/mpi/coll/op/op*.c via MPIR_OP_TYPE_REDUCE_CASE,
+// src/include/mpir_op_util.h:48-55).  Declared in include/mpir_hip_reduce.h.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "mpir_hip_reduce.h"
+#include "reduce_kernels.hpp"
+
+using namespace mpir_hip;
+
+namespace {
+
+typedef hipError_t (*launch_fn)(const void *, void *, uint64_t, hipStream_t);
+
+struct Entry { launch_fn fn; };
+Entry g_table[MPIR_HIP_NOPS][MPIR_HIP_NELEMS];
+
+template <class Op, class T>
+void reg(int op, int elem) { g_table[op][elem].fn = &launch_reduce<Op, T>; }
+
+// Integer element classes and their device types.
+#define FOR_INTS(X) \
+    X(MPIR_HIP_I8, int8_t) X(MPIR_HIP_U8, uint8_t) X(MPIR_HIP_I16, int16_t) X(MPIR_HIP_U16, uint16_t) \
+    X(MPIR_HIP_I32, int32_t) X(MPIR_HIP_U32, uint32_t) X(MPIR_HIP_I64, int64_t) X(MPIR_HIP_U64, uint64_t)
+#define FOR_REALS(X) X(MPIR_HIP_F16, f16) X(MPIR_HIP_F32, float) X(MPIR_HIP_F64, double)
+#define FOR_CPLX(X) X(MPIR_HIP_CF32, cf32) X(MPIR_HIP_CF64, cf64)
+#define FOR_PAIRS(X) \
+    X(MPIR_HIP_P2INT, p2int) X(MPIR_HIP_PFLOATINT, pfloatint) X(MPIR_HIP_PLONGINT, plongint) \
+    X(MPIR_HIP_PSHORTINT, pshortint) X(MPIR_HIP_PDOUBLEINT, pdoubleint)
+
+struct TableInit {
+    TableInit() {
+        memset(g_table, 0, sizeof(g_table));
+        // SUM / PROD: C_INTEGER, FORTRAN_INTEGER, FLOATING_POINT (+EXTRA: char, _Float16), COMPLEX
+#define X(E, T) reg<OpSum, T>(MPIR_HIP_OP_SUM, E); reg<OpProd, T>(MPIR_HIP_OP_PROD, E);
+        FOR_INTS(X) FOR_REALS(X) FOR_CPLX(X)
+#undef X
+        // MAX / MIN: integers and reals, no complex
+#define X(E, T) reg<OpMax, T>(MPIR_HIP_OP_MAX, E); reg<OpMin, T>(MPIR_HIP_OP_MIN, E);
+        FOR_INTS(X) FOR_REALS(X)
+#undef X
+        // LAND / LOR: integers (+ _Bool as u8); LXOR also reals (oplxor.c:66-67)
+#define X(E, T) reg<OpLand, T>(MPIR_HIP_OP_LAND, E); reg<OpLor, T>(MPIR_HIP_OP_LOR, E); \
+                reg<OpLxor, T>(MPIR_HIP_OP_LXOR, E);
+        FOR_INTS(X)
+#undef X
+#define X(E, T) reg<OpLxor, T>(MPIR_HIP_OP_LXOR, E);
+        FOR_REALS(X)
+#undef X
+        // BAND / BOR / BXOR: integers and byte
+#define X(E, T) reg<OpBand, T>(MPIR_HIP_OP_BAND, E); reg<OpBor, T>(MPIR_HIP_OP_BOR, E); \
+                reg<OpBxor, T>(MPIR_HIP_OP_BXOR, E);
+        FOR_INTS(X)
+#undef X
+        // MAXLOC / MINLOC: pair types
+#define X(E, T) reg<OpMaxloc, T>(MPIR_HIP_OP_MAXLOC, E); reg<OpMinloc, T>(MPIR_HIP_OP_MINLOC, E);
+        FOR_PAIRS(X)
+#undef X
+        // REPLACE: a byte copy for every class (MPIR_Localcopy of a basic type)
+        for (int e = 1; e < MPIR_HIP_NELEMS; ++e) reg<OpReplace, uint8_t>(MPIR_HIP_OP_REPLACE, e);
+    }
+} g_table_init;
+
+const size_t g_elem_size[MPIR_HIP_NELEMS] = {
+    0, 1, 1, 2, 2, 4, 4, 8, 8, 2, 4, 8, 8, 16, 8, 8, 16, 8, 16,
+};
+
+// ------------------------------------------------------------ per-thread state
+constexpr int kMaxDev = 64;
+constexpr uint64_t kStageChunk = 64ull << 20;  // bytes per operand per staging chunk
+
+struct DevCtx {
+    hipStream_t stream[2] = {nullptr, nullptr};
+    char *scratch = nullptr;     // 2 slots x (in, inout) x kStageChunk
+    size_t scratch_bytes = 0;
+};
+
+struct ThreadCtx {
+    DevCtx dev[kMaxDev];
+    char err[256] = {0};
+};
+
+thread_local ThreadCtx t_ctx;
+
+int set_err(hipError_t e, const char *what) {
+    snprintf(t_ctx.err, sizeof(t_ctx.err), "%s: %s", what, hipGetErrorString(e));
+    return MPIR_HIP_ERUNTIME;
+}
+
+#define HIPCHK(call) do { hipError_t e_ = (call); if (e_ != hipSuccess) return set_err(e_, #call); } while (0)
+
+int get_stream(int dev, int slot, hipStream_t *out) {
+    DevCtx &d = t_ctx.dev[dev];
+    if (!d.stream[slot]) {
+        // Blocking stream (not hipStreamNonBlocking): it orders after work the
+        // caller queued on the legacy null stream for these buffers.
+        HIPCHK(hipStreamCreate(&d.stream[slot]));
+    }
+    *out = d.stream[slot];
+    return MPIR_HIP_OK;
+}
+
+int get_scratch(int dev, size_t bytes, char **out) {
+    DevCtx &d = t_ctx.dev[dev];
+    if (d.scratch_bytes < bytes) {
+        if (d.scratch) HIPCHK(hipFree(d.scratch));
+        d.scratch = nullptr;
+        d.scratch_bytes = 0;
+        HIPCHK(hipMalloc(&d.scratch, bytes));
+        d.scratch_bytes = bytes;
+    }
+    *out = d.scratch;
+    return MPIR_HIP_OK;
+}
+
+enum Loc { LOC_HOST = 0, LOC_DEVICE = 1 };
+
+// Device memory (hipMalloc, managed) is combined in place; anything else
+// (pageable or pinned host memory) is staged through device scratch.
+Loc classify(const void *p, int *dev) {
+    hipPointerAttribute_t at;
+    hipError_t e = hipPointerGetAttributes(&at, p);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        return LOC_HOST;
+    }
+    if (at.type == hipMemoryTypeDevice || at.type == hipMemoryTypeManaged || at.type == hipMemoryTypeUnified) {
+        *dev = at.device;
+        return LOC_DEVICE;
+    }
+    return LOC_HOST;
+}
+
+int wait_stream(hipStream_t s) {
+    HIPCHK(hipStreamSynchronize(s));
+    return MPIR_HIP_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+size_t MPIR_Hip_elem_size(int elem) {
+    return (elem > 0 && elem < MPIR_HIP_NELEMS) ? g_elem_size[elem] : 0;
+}
+
+int MPIR_Hip_has_kernel(int op, int elem) {
+    if (op <= 0 || op >= MPIR_HIP_NOPS || elem <= 0 || elem >= MPIR_HIP_NELEMS) return 0;
+    return g_table[op][elem].fn != nullptr;
+}
+
+const char *MPIR_Hip_error_string(void) { return t_ctx.err; }
+
+int MPIR_Hip_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) { (void)hipGetLastError(); return 0; }
+    return n;
+}
+
+int MPIR_Hip_is_device_ptr(const void *p) {
+    int dev = 0;
+    return classify(p, &dev) == LOC_DEVICE;
+}
+
+int MPIR_Hip_memcpy(void *dst, const void *src, size_t bytes) {
+    if (!bytes) return MPIR_HIP_OK;
+    HIPCHK(hipMemcpy(dst, src, bytes, hipMemcpyDefault));
+    return MPIR_HIP_OK;
+}
+
+int MPIR_Hip_reduce(const void *inbuf, void *inoutbuf, uint64_t count, int op, int elem, void *hip_stream,
+                    int sync) {
+    t_ctx.err[0] = 0;
+    if (!MPIR_Hip_has_kernel(op, elem)) return MPIR_HIP_ENOKERNEL;
+    if (count == 0) return MPIR_HIP_OK;
+    launch_fn fn = g_table[op][elem].fn;
+    const size_t esz = g_elem_size[elem];
+    // REPLACE is registered as a byte copy: its launcher counts bytes
+    const uint64_t unit = (op == MPIR_HIP_OP_REPLACE) ? 1 : esz;
+
+    int din = -1, dio = -1;
+    const Loc lin = classify(inbuf, &din);
+    const Loc lio = classify(inoutbuf, &dio);
+
+    // ---- fast path: both operands device-resident on one device ----------
+    if (lin == LOC_DEVICE && lio == LOC_DEVICE && din == dio) {
+        int cur = 0;
+        HIPCHK(hipGetDevice(&cur));
+        if (cur != dio) HIPCHK(hipSetDevice(dio));
+        hipStream_t s = (hipStream_t)hip_stream;
+        int rc = MPIR_HIP_OK;
+        if (!s) rc = get_stream(dio, 0, &s);
+        if (rc == MPIR_HIP_OK) {
+            hipError_t e = fn(inbuf, inoutbuf, count * esz / unit, s);
+            if (e != hipSuccess) rc = set_err(e, "kernel launch");
+            else if (sync) rc = wait_stream(s);
+        }
+        if (cur != dio) (void)hipSetDevice(cur);
+        return rc;
+    }
+    if (!sync) return MPIR_HIP_EBUFFER;  // the stream variant needs device buffers
+
+    // ---- staged path: at least one operand is host memory (or the two ----
+    // ---- operands live on different devices).  Chunks ping-pong over  ----
+    // ---- two streams so the copies of chunk k+1 overlap chunk k.      ----
+    int dev = 0;
+    if (lio == LOC_DEVICE) dev = dio;
+    else if (lin == LOC_DEVICE) dev = din;
+    else {
+        HIPCHK(hipGetDevice(&dev));
+        if (MPIR_Hip_device_count() == 0) return MPIR_HIP_ENODEV;
+    }
+    int cur = 0;
+    HIPCHK(hipGetDevice(&cur));
+    if (cur != dev) HIPCHK(hipSetDevice(dev));
+
+    int rc = MPIR_HIP_OK;
+    const bool stage_in = !(lin == LOC_DEVICE && din == dev);
+    const bool stage_io = !(lio == LOC_DEVICE && dio == dev);
+    const uint64_t total = count * esz;
+    uint64_t chunk_elems = kStageChunk / esz;
+    if (chunk_elems > count) chunk_elems = count;
+    const uint64_t chunk_bytes = chunk_elems * esz;
+    char *scratch = nullptr;
+    hipStream_t st[2];
+    rc = get_scratch(dev, 4 * ((chunk_bytes + 255) & ~(uint64_t)255), &scratch);
+    if (rc == MPIR_HIP_OK) rc = get_stream(dev, 0, &st[0]);
+    if (rc == MPIR_HIP_OK) rc = get_stream(dev, 1, &st[1]);
+    const uint64_t slot_bytes = (chunk_bytes + 255) & ~(uint64_t)255;
+    const char *cin = static_cast<const char *>(inbuf);
+    char *cio = static_cast<char *>(inoutbuf);
+    for (uint64_t off = 0, k = 0; rc == MPIR_HIP_OK && off < total; off += chunk_bytes, ++k) {
+        const uint64_t nb = (total - off < chunk_bytes) ? total - off : chunk_bytes;
+        const int slot = (int)(k & 1);
+        hipStream_t s = st[slot];
+        char *sin = scratch + (2 * slot) * slot_bytes;
+        char *sio = scratch + (2 * slot + 1) * slot_bytes;
+        const void *kin = cin + off;
+        void *kio = cio + off;
+        hipError_t e = hipSuccess;
+        if (stage_in) { e = hipMemcpyAsync(sin, cin + off, nb, hipMemcpyDefault, s); kin = sin; }
+        if (e == hipSuccess && stage_io) { e = hipMemcpyAsync(sio, cio + off, nb, hipMemcpyDefault, s); kio = sio; }
+        if (e == hipSuccess) e = fn(kin, kio, nb / unit, s);
+        if (e == hipSuccess && stage_io) e = hipMemcpyAsync(cio + off, sio, nb, hipMemcpyDefault, s);
+        if (e != hipSuccess) rc = set_err(e, "staged reduce");
+    }
+    if (rc == MPIR_HIP_OK) rc = wait_stream(st[0]);
+    if (rc == MPIR_HIP_OK) rc = wait_stream(st[1]);
+    if (cur != dev) (void)hipSetDevice(cur);
+    return rc;
+}
+
+}  // extern "C"

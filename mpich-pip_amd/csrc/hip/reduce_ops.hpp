@@ -1,0 +1,165 @@
+// reduce_ops.hpp -- element combine functors for the MPI_Op x basic-type matrix.
+//
+// Each functor computes the new inout element from (a = inout, b = in), i.e.
+// the body of MPIR_OP_TYPE_REDUCE_CASE `a[i] = op_macro_(a[i], b[i])`
+// (reference src/include/mpir_op_util.h:48-55).  The semantics are those of
+// the reference's x86-64 C loops, restated for gfx950:
+//   * integers: two's-complement wraparound (the reference's signed overflow
+//     wraps in practice; short/char are promoted then truncated) -> computed
+//     in the unsigned type of the same width, bit-identical.
+//   * MAX/MIN: compare-select exactly like MPL_MAX/MPL_MIN
+//     (src/mpl/include/mpl_base.h:124-125): MAX = (a > b) ? a : b.  With an
+//     unordered compare or equality the result is b (the inbuf element), so
+//     NaN and signed-zero results match the reference.  Never v_max_f32.
+//   * floating point: one IEEE round-to-nearest-even operation per element,
+//     denormals preserved, no contraction (the TU is built -ffp-contract=off).
+//   * C _Complex PROD: the C99 Annex G multiply (the inline fast path plus the
+//     NaN-recovery branch of __mulsc3/__muldc3 that gcc/clang call).
+//   * LAND/LOR/LXOR: result is 0/1 converted to the element type
+//     (oplxor.c:26 `((a)&&(!b))||((!a)&&(b))`).
+//   * MAXLOC/MINLOC: opmaxloc.c:48-59 / opminloc.c:48-59 -- take the winning
+//     pair; on equality loc = MPL_MIN(loc_a, loc_b); padding bytes untouched.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace mpir_hip {
+
+typedef _Float16 f16;
+
+struct cf32 { float re, im; };
+struct cf64 { double re, im; };
+
+// MAXLOC/MINLOC pair layouts on x86-64 (opmaxloc.c:14-40)
+struct p2int     { int32_t value; int32_t loc; };                    //  8 B
+struct pfloatint { float value; int32_t loc; };                      //  8 B
+struct plongint  { int64_t value; int32_t loc; int32_t pad_; };      // 16 B
+struct pshortint { int16_t value; int16_t pad_; int32_t loc; };      //  8 B
+struct pdoubleint{ double value; int32_t loc; int32_t pad_; };       // 16 B
+
+template <class T> struct uns { typedef T type; };
+template <> struct uns<int8_t>  { typedef uint8_t  type; };
+template <> struct uns<int16_t> { typedef uint16_t type; };
+template <> struct uns<int32_t> { typedef uint32_t type; };
+template <> struct uns<int64_t> { typedef uint64_t type; };
+
+// ---------------------------------------------------------------- arithmetic
+struct OpSum {
+    template <class T> __device__ __forceinline__ T operator()(T a, T b) const {
+        typedef typename uns<T>::type U;
+        return (T)(U)((U)a + (U)b);
+    }
+    __device__ __forceinline__ f16 operator()(f16 a, f16 b) const { return a + b; }
+    __device__ __forceinline__ float operator()(float a, float b) const { return a + b; }
+    __device__ __forceinline__ double operator()(double a, double b) const { return a + b; }
+    __device__ __forceinline__ cf32 operator()(cf32 a, cf32 b) const { return cf32{a.re + b.re, a.im + b.im}; }
+    __device__ __forceinline__ cf64 operator()(cf64 a, cf64 b) const { return cf64{a.re + b.re, a.im + b.im}; }
+};
+
+// C99 Annex G complex multiply (a + ib) * (c + id), as emitted by gcc/clang
+// for `_Complex` operands: fast path, then the __mul?c3 recovery when both
+// parts come out NaN.  Kept out of line-of-sight of contraction by the build.
+template <class R>
+__device__ __forceinline__ void annexg_mul(R a, R b, R c, R d, R &x, R &y) {
+    R ac = a * c, bd = b * d, ad = a * d, bc = b * c;
+    x = ac - bd;
+    y = ad + bc;
+    if (__builtin_expect(__builtin_isnan(x) && __builtin_isnan(y), 0)) {
+        bool recalc = false;
+        if (__builtin_isinf(a) || __builtin_isinf(b)) {
+            a = __builtin_copysign(__builtin_isinf(a) ? (R)1 : (R)0, a);
+            b = __builtin_copysign(__builtin_isinf(b) ? (R)1 : (R)0, b);
+            if (__builtin_isnan(c)) c = __builtin_copysign((R)0, c);
+            if (__builtin_isnan(d)) d = __builtin_copysign((R)0, d);
+            recalc = true;
+        }
+        if (__builtin_isinf(c) || __builtin_isinf(d)) {
+            c = __builtin_copysign(__builtin_isinf(c) ? (R)1 : (R)0, c);
+            d = __builtin_copysign(__builtin_isinf(d) ? (R)1 : (R)0, d);
+            if (__builtin_isnan(a)) a = __builtin_copysign((R)0, a);
+            if (__builtin_isnan(b)) b = __builtin_copysign((R)0, b);
+            recalc = true;
+        }
+        if (!recalc && (__builtin_isinf(ac) || __builtin_isinf(bd) || __builtin_isinf(ad) || __builtin_isinf(bc))) {
+            if (__builtin_isnan(a)) a = __builtin_copysign((R)0, a);
+            if (__builtin_isnan(b)) b = __builtin_copysign((R)0, b);
+            if (__builtin_isnan(c)) c = __builtin_copysign((R)0, c);
+            if (__builtin_isnan(d)) d = __builtin_copysign((R)0, d);
+            recalc = true;
+        }
+        if (recalc) {
+            x = (R)__builtin_inf() * (a * c - b * d);
+            y = (R)__builtin_inf() * (a * d + b * c);
+        }
+    }
+}
+
+struct OpProd {
+    template <class T> __device__ __forceinline__ T operator()(T a, T b) const {
+        typedef typename uns<T>::type U;
+        return (T)(U)((U)a * (U)b);
+    }
+    __device__ __forceinline__ f16 operator()(f16 a, f16 b) const { return a * b; }
+    __device__ __forceinline__ float operator()(float a, float b) const { return a * b; }
+    __device__ __forceinline__ double operator()(double a, double b) const { return a * b; }
+    __device__ __forceinline__ cf32 operator()(cf32 a, cf32 b) const {
+        cf32 r; annexg_mul<float>(a.re, a.im, b.re, b.im, r.re, r.im); return r;
+    }
+    __device__ __forceinline__ cf64 operator()(cf64 a, cf64 b) const {
+        cf64 r; annexg_mul<double>(a.re, a.im, b.re, b.im, r.re, r.im); return r;
+    }
+};
+
+// MPL_MAX(a,b) (((a) > (b)) ? (a) : (b)); a = inout, b = in
+struct OpMax {
+    template <class T> __device__ __forceinline__ T operator()(T a, T b) const { return (a > b) ? a : b; }
+};
+struct OpMin {
+    template <class T> __device__ __forceinline__ T operator()(T a, T b) const { return (a < b) ? a : b; }
+};
+
+// ---------------------------------------------------------------- logical
+template <class T> __device__ __forceinline__ bool truth(T v) { return v != (T)0; }
+
+struct OpLand {
+    template <class T> __device__ __forceinline__ T operator()(T a, T b) const { return (T)(truth(a) && truth(b)); }
+};
+struct OpLor {
+    template <class T> __device__ __forceinline__ T operator()(T a, T b) const { return (T)(truth(a) || truth(b)); }
+};
+struct OpLxor {
+    template <class T> __device__ __forceinline__ T operator()(T a, T b) const {
+        return (T)((truth(a) && !truth(b)) || (!truth(a) && truth(b)));
+    }
+};
+
+// ---------------------------------------------------------------- bitwise
+struct OpBand { template <class T> __device__ __forceinline__ T operator()(T a, T b) const { return (T)(a & b); } };
+struct OpBor  { template <class T> __device__ __forceinline__ T operator()(T a, T b) const { return (T)(a | b); } };
+struct OpBxor { template <class T> __device__ __forceinline__ T operator()(T a, T b) const { return (T)(a ^ b); } };
+
+// ---------------------------------------------------------------- loc pairs
+// opmaxloc.c:48-59: if (a.value < b.value) a = b;
+//                   else if (a.value <= b.value) a.loc = MPL_MIN(a.loc, b.loc);
+struct OpMaxloc {
+    template <class P> __device__ __forceinline__ P operator()(P a, P b) const {
+        if (a.value < b.value) { a.value = b.value; a.loc = b.loc; }
+        else if (a.value <= b.value) a.loc = (a.loc < b.loc) ? a.loc : b.loc;
+        return a;
+    }
+};
+// opminloc.c:48-59 (mirror with > / >=)
+struct OpMinloc {
+    template <class P> __device__ __forceinline__ P operator()(P a, P b) const {
+        if (a.value > b.value) { a.value = b.value; a.loc = b.loc; }
+        else if (a.value >= b.value) a.loc = (a.loc < b.loc) ? a.loc : b.loc;
+        return a;
+    }
+};
+
+// REPLACE (opreplace.c:15 -> MPIR_Localcopy): inout = in
+struct OpReplace {
+    template <class T> __device__ __forceinline__ T operator()(T, T b) const { return b; }
+};
+
+}  // namespace mpir_hip

@@ -1,0 +1,183 @@
+"""ctypes binding of libmpich_reduce_local.so -- the MI355X MPI_Reduce_local.
+
+This is host plumbing for tests, the benchmark and the smoke check; the
+product is the C ABI declared in include/mpi_reduce_local.h (see
+INTEGRATION.md for how MPICH links it).  Constants mirror that header, which
+mirrors the reference's mpi.h.in / configure.ac values.
+
+The library is loaded from mpich-pip_amd/lib/ (built by `make -C
+mpich-pip_amd` or __graft_entry__.build()).  A missing library raises
+immediately: there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", "libmpich_reduce_local.so")
+
+# ---- error classes (mpi.h.in:784-811)
+MPI_SUCCESS = 0
+MPI_ERR_BUFFER = 1
+MPI_ERR_COUNT = 2
+MPI_ERR_TYPE = 3
+MPI_ERR_OP = 9
+MPI_ERR_ARG = 12
+MPI_ERR_OTHER = 15
+
+MPI_ERRORS_ARE_FATAL = 0x54000000
+MPI_ERRORS_RETURN = 0x54000001
+
+# ---- ops (mpi.h.in:310-325)
+MPI_OP_NULL = 0x18000000
+MPI_MAX = 0x58000001
+MPI_MIN = 0x58000002
+MPI_SUM = 0x58000003
+MPI_PROD = 0x58000004
+MPI_LAND = 0x58000005
+MPI_BAND = 0x58000006
+MPI_LOR = 0x58000007
+MPI_BOR = 0x58000008
+MPI_LXOR = 0x58000009
+MPI_BXOR = 0x5800000A
+MPI_MINLOC = 0x5800000B
+MPI_MAXLOC = 0x5800000C
+MPI_REPLACE = 0x5800000D
+MPI_NO_OP = 0x5800000E
+
+OPS = {
+    "MPI_MAX": MPI_MAX, "MPI_MIN": MPI_MIN, "MPI_SUM": MPI_SUM, "MPI_PROD": MPI_PROD,
+    "MPI_LAND": MPI_LAND, "MPI_BAND": MPI_BAND, "MPI_LOR": MPI_LOR, "MPI_BOR": MPI_BOR,
+    "MPI_LXOR": MPI_LXOR, "MPI_BXOR": MPI_BXOR, "MPI_MINLOC": MPI_MINLOC, "MPI_MAXLOC": MPI_MAXLOC,
+}
+
+# ---- datatypes, x86-64 values (configure.ac:3442-3705)
+MPI_DATATYPE_NULL = 0x0C000000
+DATATYPES = {
+    "MPI_CHAR": 0x4C000101,
+    "MPI_UNSIGNED_CHAR": 0x4C000102,
+    "MPI_SHORT": 0x4C000203,
+    "MPI_UNSIGNED_SHORT": 0x4C000204,
+    "MPI_INT": 0x4C000405,
+    "MPI_UNSIGNED": 0x4C000406,
+    "MPI_LONG": 0x4C000807,
+    "MPI_UNSIGNED_LONG": 0x4C000808,
+    "MPI_LONG_LONG": 0x4C000809,
+    "MPI_FLOAT": 0x4C00040A,
+    "MPI_DOUBLE": 0x4C00080B,
+    "MPI_BYTE": 0x4C00010D,
+    "MPI_WCHAR": 0x4C00040E,
+    "MPI_2INT": 0x4C000816,
+    "MPI_SIGNED_CHAR": 0x4C000118,
+    "MPI_UNSIGNED_LONG_LONG": 0x4C000819,
+    "MPI_FLOAT_INT": 0x8C000000,
+    "MPI_DOUBLE_INT": 0x8C000001,
+    "MPI_LONG_INT": 0x8C000002,
+    "MPI_SHORT_INT": 0x8C000003,
+    "MPI_INT8_T": 0x4C000137,
+    "MPI_INT16_T": 0x4C000238,
+    "MPI_INT32_T": 0x4C000439,
+    "MPI_INT64_T": 0x4C00083A,
+    "MPI_UINT8_T": 0x4C00013B,
+    "MPI_UINT16_T": 0x4C00023C,
+    "MPI_UINT32_T": 0x4C00043D,
+    "MPI_UINT64_T": 0x4C00083E,
+    "MPI_C_BOOL": 0x4C00013F,
+    "MPI_C_FLOAT_COMPLEX": 0x4C000840,
+    "MPI_C_DOUBLE_COMPLEX": 0x4C001041,
+    "MPIX_C_FLOAT16": 0x4C000246,
+    "MPI_AINT": 0x4C000843,
+    "MPI_OFFSET": 0x4C000844,
+    "MPI_COUNT": 0x4C000845,
+}
+globals().update(DATATYPES)
+
+# Every symbol include/mpi_reduce_local.h declares (checked by the CPU tests).
+EXPORTED_SYMBOLS = [
+    "MPI_Reduce_local", "PMPI_Reduce_local", "MPIR_Reduce_local",
+    "MPIR_MAXF", "MPIR_MINF", "MPIR_SUM", "MPIR_PROD", "MPIR_LAND", "MPIR_BAND", "MPIR_LOR",
+    "MPIR_BOR", "MPIR_LXOR", "MPIR_BXOR", "MPIR_MAXLOC", "MPIR_MINLOC", "MPIR_REPLACE", "MPIR_NO_OP",
+    "MPIR_MAXF_check_dtype", "MPIR_MINF_check_dtype", "MPIR_SUM_check_dtype", "MPIR_PROD_check_dtype",
+    "MPIR_LAND_check_dtype", "MPIR_BAND_check_dtype", "MPIR_LOR_check_dtype", "MPIR_BOR_check_dtype",
+    "MPIR_LXOR_check_dtype", "MPIR_BXOR_check_dtype", "MPIR_MAXLOC_check_dtype",
+    "MPIR_MINLOC_check_dtype", "MPIR_REPLACE_check_dtype", "MPIR_NO_OP_check_dtype",
+    "MPIR_Op_table", "MPIR_Op_check_dtype_table",
+    "MPI_Op_create", "PMPI_Op_create", "MPI_Op_free", "PMPI_Op_free",
+    "MPI_Op_commutative", "PMPI_Op_commutative", "MPIR_Op_is_commutative",
+    "MPI_Error_class", "MPI_Error_string",
+    "MPIX_Reduce_local_stream", "MPIX_Reduce_local_set_errhandler", "MPIX_Reduce_local_get_errhandler",
+    # the HIP shim (include/mpir_hip_reduce.h)
+    "MPIR_Hip_reduce", "MPIR_Hip_elem_size", "MPIR_Hip_has_kernel", "MPIR_Hip_is_device_ptr",
+    "MPIR_Hip_memcpy", "MPIR_Hip_error_string", "MPIR_Hip_device_count",
+]
+
+MPI_User_function = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_void_p,
+                                     ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int))
+
+_lib = None
+
+
+def load(path: str | None = None) -> ctypes.CDLL:
+    """Load the C-ABI library (raises if it was not built)."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = path or LIB_PATH
+    if not os.path.exists(p):
+        raise RuntimeError(f"{p} missing: build it with `make -C mpich-pip_amd` "
+                           "(no CPU fallback exists for MPI_Reduce_local)")
+    lib = ctypes.CDLL(p, mode=ctypes.RTLD_GLOBAL)
+    vp, i32 = ctypes.c_void_p, ctypes.c_int
+    for name in ("MPI_Reduce_local", "PMPI_Reduce_local", "MPIR_Reduce_local"):
+        f = getattr(lib, name)
+        f.argtypes = [vp, vp, i32, i32, i32]
+        f.restype = i32
+    lib.MPIX_Reduce_local_stream.argtypes = [vp, vp, i32, i32, i32, vp]
+    lib.MPIX_Reduce_local_stream.restype = i32
+    lib.MPIX_Reduce_local_set_errhandler.argtypes = [i32]
+    lib.MPIX_Reduce_local_set_errhandler.restype = i32
+    lib.MPI_Op_create.argtypes = [MPI_User_function, i32, ctypes.POINTER(i32)]
+    lib.MPI_Op_create.restype = i32
+    lib.MPI_Op_free.argtypes = [ctypes.POINTER(i32)]
+    lib.MPI_Op_free.restype = i32
+    lib.MPI_Op_commutative.argtypes = [i32, ctypes.POINTER(i32)]
+    lib.MPI_Op_commutative.restype = i32
+    lib.MPIR_Op_is_commutative.argtypes = [i32]
+    lib.MPIR_Op_is_commutative.restype = i32
+    lib.MPI_Error_string.argtypes = [i32, ctypes.c_char_p, ctypes.POINTER(i32)]
+    lib.MPI_Error_string.restype = i32
+    lib.MPIR_Hip_reduce.argtypes = [vp, vp, ctypes.c_uint64, i32, i32, vp, i32]
+    lib.MPIR_Hip_reduce.restype = i32
+    lib.MPIR_Hip_has_kernel.argtypes = [i32, i32]
+    lib.MPIR_Hip_has_kernel.restype = i32
+    lib.MPIR_Hip_elem_size.argtypes = [i32]
+    lib.MPIR_Hip_elem_size.restype = ctypes.c_size_t
+    lib.MPIR_Hip_device_count.restype = i32
+    lib.MPIR_Hip_error_string.restype = ctypes.c_char_p
+    for name in [n for n in EXPORTED_SYMBOLS if n.endswith("_check_dtype")]:
+        f = getattr(lib, name)
+        f.argtypes = [i32]
+        f.restype = i32
+    if path is None:
+        _lib = lib
+    return lib
+
+
+def error_string(code: int) -> str:
+    lib = load()
+    buf = ctypes.create_string_buffer(512)
+    n = ctypes.c_int(0)
+    lib.MPI_Error_string(code, buf, ctypes.byref(n))
+    return buf.value.decode(errors="replace")
+
+
+def reduce_local(inbuf: int, inoutbuf: int, count: int, datatype: int, op: int) -> int:
+    """MPI_Reduce_local on raw addresses (device or host)."""
+    return load().MPI_Reduce_local(ctypes.c_void_p(inbuf), ctypes.c_void_p(inoutbuf), count, datatype, op)
+
+
+def reduce_local_stream(inbuf: int, inoutbuf: int, count: int, datatype: int, op: int, stream: int = 0) -> int:
+    """MPIX_Reduce_local_stream: enqueue on a HIP stream (0 = library stream), no wait."""
+    return load().MPIX_Reduce_local_stream(ctypes.c_void_p(inbuf), ctypes.c_void_p(inoutbuf), count,
+                                           datatype, op, ctypes.c_void_p(stream or None))

@@ -1,0 +1,55 @@
+"""ctypes binding of the CPU oracle (oracle/liboracle.so).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and
+bench.py's cpu_baseline leg as the checker / CPU baseline, never by the
+product library (mpich-pip_amd/).  See op_oracle.c for what it restates.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "liboracle.so")
+_lib = None
+
+
+def load() -> ctypes.CDLL:
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"{LIB_PATH} missing: run `make -C oracle`")
+        lib = ctypes.CDLL(LIB_PATH)
+        vp, i32 = ctypes.c_void_p, ctypes.c_int
+        for name in ("oracle_reduce_local", "oracle_reduce_local_nocheck"):
+            f = getattr(lib, name)
+            f.argtypes = [vp, vp, i32, i32, i32]
+            f.restype = i32
+        lib.oracle_check_dtype.argtypes = [i32, i32]
+        lib.oracle_check_dtype.restype = i32
+        lib.oracle_cpu_baseline_sum_f32.argtypes = [i32, ctypes.c_long, i32]
+        lib.oracle_cpu_baseline_sum_f32.restype = ctypes.c_double
+        lib.oracle_h2f.argtypes = [ctypes.c_uint16]
+        lib.oracle_h2f.restype = ctypes.c_float
+        lib.oracle_f2h.argtypes = [ctypes.c_float]
+        lib.oracle_f2h.restype = ctypes.c_uint16
+        _lib = lib
+    return _lib
+
+
+def reduce_local(inbuf, inoutbuf, count: int, datatype: int, op: int, check: bool = True) -> int:
+    """Oracle MPI_Reduce_local on numpy arrays (or raw addresses); inoutbuf updated in place."""
+    lib = load()
+    pin = inbuf.ctypes.data if hasattr(inbuf, "ctypes") else inbuf
+    pio = inoutbuf.ctypes.data if hasattr(inoutbuf, "ctypes") else inoutbuf
+    fn = lib.oracle_reduce_local if check else lib.oracle_reduce_local_nocheck
+    return fn(ctypes.c_void_p(pin), ctypes.c_void_p(pio), count, datatype, op)
+
+
+def check_dtype(op: int, datatype: int) -> int:
+    return load().oracle_check_dtype(op, datatype)
+
+
+def cpu_baseline_sum_f32(nthreads: int, count: int, iters: int) -> float:
+    """Seconds taken by the slowest of `nthreads` threads doing `iters` fp32 SUM calls of `count`."""
+    return load().oracle_cpu_baseline_sum_f32(nthreads, count, iters)

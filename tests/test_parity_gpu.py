@@ -1,0 +1,232 @@
+"""GPU parity: the gfx950 MPI_Reduce_local against the CPU oracle (MI355X).
+
+Every call goes through the C ABI (MPI_Reduce_local / MPIX_Reduce_local_stream
+in libmpich_reduce_local.so) with device buffers allocated by torch (plumbing
+only).  The bar is bit-exact for every op and type -- each element is one
+IEEE round-to-nearest-even operation on both sides (SURVEY.md §8c
+'Tolerance') -- so outputs are compared as bytes.
+"""
+import ctypes
+import json
+import os
+
+import numpy as np
+import pytest
+
+import _types as T
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def dev(torch, host_bytes: np.ndarray, offset: int = 0):
+    """Copy bytes to a fresh device allocation at `offset`; returns (tensor, address)."""
+    n = host_bytes.size
+    t = torch.zeros(n + offset + 256, dtype=torch.uint8, device="cuda")
+    if n:
+        t[offset:offset + n].copy_(torch.from_numpy(np.ascontiguousarray(host_bytes)))
+    torch.cuda.synchronize()
+    return t, t.data_ptr() + offset
+
+
+def back(t, offset, n):
+    import torch
+    torch.cuda.synchronize()
+    return t[offset:offset + n].cpu().numpy()
+
+
+def explain(got, want, a, b, esz, limit=6):
+    g = got.reshape(-1, esz)
+    w = want.reshape(-1, esz)
+    bad = np.nonzero((g != w).any(axis=1))[0]
+    lines = [f"{bad.size} of {g.shape[0]} elements differ"]
+    for i in bad[:limit]:
+        lines.append(f"  [{i}] inout={a.reshape(-1, esz)[i].tobytes()[::-1].hex()} in={b.reshape(-1, esz)[i].tobytes()[::-1].hex()}"
+                     f" gpu={g[i].tobytes()[::-1].hex()} oracle={w[i].tobytes()[::-1].hex()}")
+    return "\n".join(lines)
+
+
+def run_pair(mpi, orc, torch, op, t, n, seed, off_in=0, off_io=0):
+    rng = np.random.default_rng(seed)
+    a = T.to_bytes(T.gen(t, n, rng, op))          # inout
+    b = T.to_bytes(T.gen(t, n, rng, op))          # in
+    want = a.copy()
+    rc_o = orc.reduce_local(b.copy(), want, n, mpi.DATATYPES[t], mpi.OPS[op])
+    tio, pio = dev(torch, a, off_io)
+    tin, pin = dev(torch, b, off_in)
+    rc = mpi.reduce_local(pin, pio, n, mpi.DATATYPES[t], mpi.OPS[op])
+    got = back(tio, off_io, a.size)
+    assert rc == rc_o, (op, t, rc, rc_o)
+    assert np.array_equal(back(tin, off_in, b.size), b), "inbuf modified"
+    if not np.array_equal(got, want):
+        pytest.fail(f"{op} {t} n={n} off=({off_in},{off_io}):\n" + explain(got, want, a, b, T.elem_size(t)))
+
+
+MATRIX = [(op, t) for op in T.OPS for t in T.ALL_TYPES if T.check_ok(op, t)]
+
+
+@pytest.mark.parametrize("op,t", MATRIX, ids=[f"{o}-{t}" for o, t in MATRIX])
+def test_matrix_vs_oracle(mpi, orc, cuda, op, t):
+    """Every (op, type) the reference accepts, edge values included, ragged counts."""
+    for n, seed in ((1, 1), (7, 2), (1000, 3), (65536 + 13, 4)):
+        run_pair(mpi, orc, cuda, op, t, n, seed)
+
+
+@pytest.mark.parametrize("t", ["MPI_FLOAT", "MPI_UNSIGNED_CHAR", "MPIX_C_FLOAT16", "MPI_DOUBLE",
+                               "MPI_C_DOUBLE_COMPLEX", "MPI_SHORT_INT", "MPI_LONG_INT"])
+def test_alignment_offsets(mpi, orc, cuda, t):
+    """Sub-range displacements: equal and unequal misalignment of in / inout mod 16."""
+    op = "MPI_MAXLOC" if t in T.PAIRS else "MPI_SUM"
+    esz = T.elem_size(t)
+    for off_in, off_io in ((0, 0), (esz, esz), (esz, 0), (0, 3 * esz), (8, 8), (4, 12), (1, 1), (3, 5)):
+        for n in (1, 5, 33, 4099):
+            run_pair(mpi, orc, cuda, op, t, n, 100 + n + off_in, off_in, off_io)
+
+
+def test_golden_kat_fold_on_gpu(mpi, cuda):
+    """The reference's own known-answer tests, folded on the GPU, bit for bit."""
+    torch = cuda
+    man = json.load(open(os.path.join(GOLD, "kat_reference.json")))["cases"]
+    data = np.load(os.path.join(GOLD, "kat_reference.npz"))
+    bad = []
+    for c in man:
+        ranks = data[c["key"] + "_ranks"]
+        sol = data[c["key"] + "_sol"]
+        dr = torch.from_numpy(ranks.copy()).cuda()
+        acc = dr[0].clone()
+        for r in range(1, c["p"]):
+            rc = mpi.reduce_local(dr[r].data_ptr(), acc.data_ptr(), c["count"], c["handle"], c["op_handle"])
+            assert rc == 0, c["id"]
+        if not np.array_equal(acc.cpu().numpy(), sol):
+            bad.append(c["id"])
+    assert not bad, f"{len(bad)} of {len(man)} KAT cases differ, e.g. {bad[:6]}"
+
+
+def test_survey_probes_on_gpu(mpi, cuda):
+    torch = cuda
+    for c in json.load(open(os.path.join(GOLD, "probe_survey.json")))["cases"]:
+        w = c["width"]
+        dt = {1: np.uint8, 2: np.uint16, 4: np.uint32, 8: np.uint64}[w]
+        io = np.array(c["inout"], dtype=dt)
+        src = np.array(c["in"], dtype=dt)
+        tio, pio = dev(torch, io.view(np.uint8))
+        tin, pin = dev(torch, src.view(np.uint8))
+        rc = mpi.reduce_local(pin, pio, len(io), mpi.DATATYPES[c["datatype"]], mpi.OPS[c["op"]])
+        got = back(tio, 0, io.nbytes).view(dt)
+        assert rc == c.get("expect_rc", 0), c["id"]
+        assert [int(x) for x in got] == c["expect"], c["id"]
+
+
+@pytest.mark.parametrize("where", ["host-host", "host-dev", "dev-host", "pinned-pinned", "pinned-dev"])
+def test_host_and_mixed_pointers(mpi, orc, cuda, where):
+    """Rank buffers that arrive in host memory (PiP shm) are staged through the GPU."""
+    torch = cuda
+    for n, t, op in ((1000, "MPI_FLOAT", "MPI_SUM"), (3 * (16 << 20) + 5, "MPI_INT", "MPI_MAX"),
+                     (777, "MPI_DOUBLE_INT", "MPI_MINLOC")):
+        rng = np.random.default_rng(n)
+        a = T.to_bytes(T.gen(t, n, rng, op))
+        b = T.to_bytes(T.gen(t, n, rng, op))
+        want = a.copy()
+        assert orc.reduce_local(b.copy(), want, n, mpi.DATATYPES[t], mpi.OPS[op]) == 0
+        src_kind, dst_kind = where.split("-")
+
+        def make(x, kind):
+            if kind == "dev":
+                tt, p = dev(torch, x)
+                return tt, p
+            if kind == "pinned":
+                tt = torch.from_numpy(x.copy()).pin_memory()
+                return tt, tt.data_ptr()
+            h = x.copy()
+            return h, h.ctypes.data
+
+        tin, pin = make(b, src_kind)
+        tio, pio = make(a, dst_kind)
+        assert mpi.reduce_local(pin, pio, n, mpi.DATATYPES[t], mpi.OPS[op]) == 0
+        torch.cuda.synchronize()
+        got = tio.cpu().numpy()[:a.size] if hasattr(tio, "cpu") else tio
+        assert np.array_equal(got, want), (where, t, op)
+
+
+def test_stream_variant(mpi, orc, cuda):
+    torch = cuda
+    n = (1 << 20) + 3
+    rng = np.random.default_rng(11)
+    a = T.to_bytes(T.gen("MPI_FLOAT", n, rng))
+    b = T.to_bytes(T.gen("MPI_FLOAT", n, rng))
+    want = a.copy()
+    orc.reduce_local(b.copy(), want, n, mpi.MPI_FLOAT, mpi.MPI_SUM)
+    tio, pio = dev(torch, a)
+    tin, pin = dev(torch, b)
+    s = torch.cuda.Stream()
+    assert mpi.reduce_local_stream(pin, pio, n, mpi.MPI_FLOAT, mpi.MPI_SUM, s.cuda_stream) == 0
+    s.synchronize()
+    assert np.array_equal(back(tio, 0, a.size), want)
+    # host pointers are refused by the stream variant
+    h = np.zeros(16, np.float32)
+    assert mpi.reduce_local_stream(h.ctypes.data, pio, 4, mpi.MPI_FLOAT, mpi.MPI_SUM, 0) == mpi.MPI_ERR_BUFFER
+    # float LAND passes check_dtype then fails in the compute switch (op_errno)
+    assert mpi.reduce_local_stream(pin, pio, 4, mpi.MPI_FLOAT, mpi.MPI_LAND, 0) == mpi.MPI_ERR_OP
+
+
+def test_user_op_on_device_buffers(mpi, cuda):
+    torch = cuda
+    lib = mpi.load()
+
+    @mpi.MPI_User_function
+    def user_op(invec, inoutvec, lenp, dtp):
+        n = lenp[0]
+        a = np.ctypeslib.as_array(ctypes.cast(invec, ctypes.POINTER(ctypes.c_int)), (n,))
+        b = np.ctypeslib.as_array(ctypes.cast(inoutvec, ctypes.POINTER(ctypes.c_int)), (n,))
+        b[:] = 2 * b + a
+
+    op = ctypes.c_int(0)
+    assert lib.MPI_Op_create(user_op, 0, ctypes.byref(op)) == 0
+    n = 4096
+    inb = torch.arange(n, dtype=torch.int32, device="cuda")
+    io = 3 * torch.arange(n, dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()
+    assert mpi.reduce_local(inb.data_ptr(), io.data_ptr(), n, mpi.MPI_INT, op.value) == 0
+    assert torch.equal(io.cpu(), 7 * torch.arange(n, dtype=torch.int32))
+    assert lib.MPI_Op_free(ctypes.byref(op)) == 0
+
+
+@pytest.mark.parametrize("op", ["MPI_SUM", "MPI_MAX", "MPI_MIN", "MPI_PROD"])
+@pytest.mark.parametrize("t", ["MPI_INT", "MPI_INT64_T", "MPI_FLOAT", "MPI_DOUBLE"])
+def test_config3_sweep_256mib(mpi, orc, cuda, op, t):
+    """BASELINE config 3: {SUM,MAX,MIN,PROD} x {int32,int64,fp32,fp64} at 256 MiB per operand,
+    compared with the oracle over the full buffer."""
+    torch = cuda
+    esz = T.elem_size(t)
+    n = (256 << 20) // esz
+    rng = np.random.default_rng(2024)
+    a = T.to_bytes(T.gen(t, n, rng, op))
+    b = T.to_bytes(T.gen(t, n, rng, op))
+    tio, pio = dev(torch, a)
+    tin, pin = dev(torch, b)
+    assert mpi.reduce_local(pin, pio, n, mpi.DATATYPES[t], mpi.OPS[op]) == 0
+    got = back(tio, 0, a.size)
+    del tio, tin
+    assert orc.reduce_local(b, a, n, mpi.DATATYPES[t], mpi.OPS[op]) == 0
+    if not np.array_equal(got, a):
+        pytest.fail(explain(got, a, a, b, esz))
+
+
+def test_config2_64mib_repeat_idempotence(mpi, cuda):
+    """BASELINE config 2 (fp32 SUM, 64 MiB): size-independent properties --
+    x + 0 == x bitwise, and 2 accumulations of b equal oracle-free torch adds."""
+    torch = cuda
+    n = (64 << 20) // 4
+    g = torch.Generator(device="cuda").manual_seed(5)
+    x = torch.rand(n, device="cuda", generator=g) * 2 - 1
+    z = torch.zeros(n, device="cuda")
+    x0 = x.clone()
+    torch.cuda.synchronize()
+    assert mpi.reduce_local(z.data_ptr(), x.data_ptr(), n, mpi.MPI_FLOAT, mpi.MPI_SUM) == 0
+    assert torch.equal(x.view(torch.int32), x0.view(torch.int32))
+    y = torch.rand(n, device="cuda", generator=g)
+    ref = x0 + y + y          # IEEE fp32 adds in the same order
+    torch.cuda.synchronize()
+    for _ in range(2):
+        assert mpi.reduce_local(y.data_ptr(), x.data_ptr(), n, mpi.MPI_FLOAT, mpi.MPI_SUM) == 0
+    assert torch.equal(x.view(torch.int32), ref.view(torch.int32))
