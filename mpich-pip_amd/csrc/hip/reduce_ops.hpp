@@ -43,53 +43,95 @@ template <> struct uns<int16_t> { typedef uint16_t type; };
 template <> struct uns<int32_t> { typedef uint32_t type; };
 template <> struct uns<int64_t> { typedef uint64_t type; };
 
+// ---------------------------------------------------------------- NaN rule
+// The reference's loops run on x86 SSE: an operation with a NaN operand
+// returns its FIRST source operand if that is a NaN, else the second, with
+// the quiet bit set; an invalid operation (inf - inf, 0 * inf) returns the
+// "real indefinite" -0x0.8p-0 NaN (sign set).  gcc -O2 places a[i] (inout)
+// first (probed; tests/test_oracle_nan_rule.py).  gfx950's v_add/v_mul follow
+// the same rule when the compiler keeps the operand order, but LLVM is free
+// to commute or re-associate signs (it rewrote `ac - bd` as -(bd - ac) in the
+// complex multiply), so the rule is enforced explicitly after each operation.
+// On a memory-bound kernel the extra compare/selects are free.
+template <class R> struct FP;
+template <> struct FP<float> {
+    typedef uint32_t U;
+    static constexpr U quiet = 0x00400000u, indefinite = 0xffc00000u;
+};
+template <> struct FP<double> {
+    typedef uint64_t U;
+    static constexpr U quiet = 0x0008000000000000ull, indefinite = 0xfff8000000000000ull;
+};
+template <> struct FP<_Float16> {
+    typedef uint16_t U;
+    static constexpr U quiet = 0x0200u, indefinite = 0xfe00u;
+};
+
+template <class R> __device__ __forceinline__ bool isnan_(R x) { return x != x; }
+template <class R> __device__ __forceinline__ R quiet_(R x) {
+    typedef typename FP<R>::U U;
+    return __builtin_bit_cast(R, (U)(__builtin_bit_cast(U, x) | FP<R>::quiet));
+}
+template <class R> __device__ __forceinline__ R x86_result(R p, R q, R r) {
+    typedef typename FP<R>::U U;
+    if (isnan_(p)) return quiet_(p);
+    if (isnan_(q)) return quiet_(q);
+    if (isnan_(r)) return __builtin_bit_cast(R, (U)FP<R>::indefinite);
+    return r;
+}
+template <class R> __device__ __forceinline__ R xadd(R p, R q) { return x86_result(p, q, (R)(p + q)); }
+template <class R> __device__ __forceinline__ R xsub(R p, R q) { return x86_result(p, q, (R)(p - q)); }
+template <class R> __device__ __forceinline__ R xmul(R p, R q) { return x86_result(p, q, (R)(p * q)); }
+
 // ---------------------------------------------------------------- arithmetic
 struct OpSum {
     template <class T> __device__ __forceinline__ T operator()(T a, T b) const {
         typedef typename uns<T>::type U;
         return (T)(U)((U)a + (U)b);
     }
-    __device__ __forceinline__ f16 operator()(f16 a, f16 b) const { return a + b; }
-    __device__ __forceinline__ float operator()(float a, float b) const { return a + b; }
-    __device__ __forceinline__ double operator()(double a, double b) const { return a + b; }
-    __device__ __forceinline__ cf32 operator()(cf32 a, cf32 b) const { return cf32{a.re + b.re, a.im + b.im}; }
-    __device__ __forceinline__ cf64 operator()(cf64 a, cf64 b) const { return cf64{a.re + b.re, a.im + b.im}; }
+    __device__ __forceinline__ f16 operator()(f16 a, f16 b) const { return xadd(a, b); }
+    __device__ __forceinline__ float operator()(float a, float b) const { return xadd(a, b); }
+    __device__ __forceinline__ double operator()(double a, double b) const { return xadd(a, b); }
+    __device__ __forceinline__ cf32 operator()(cf32 a, cf32 b) const { return cf32{xadd(a.re, b.re), xadd(a.im, b.im)}; }
+    __device__ __forceinline__ cf64 operator()(cf64 a, cf64 b) const { return cf64{xadd(a.re, b.re), xadd(a.im, b.im)}; }
 };
 
-// C99 Annex G complex multiply (a + ib) * (c + id), as emitted by gcc/clang
-// for `_Complex` operands: fast path, then the __mul?c3 recovery when both
-// parts come out NaN.  Kept out of line-of-sight of contraction by the build.
+// C99 Annex G complex multiply (a + ib) * (c + id), as gcc emits it for
+// `_Complex` operands (probed: ac = a*c, bd = b*d, bc = b*c, x = ac - bd,
+// ad = a*d, y = ad + bc, left operand first), then the __mulsc3/__muldc3
+// recovery when both parts come out NaN.
 template <class R>
 __device__ __forceinline__ void annexg_mul(R a, R b, R c, R d, R &x, R &y) {
-    R ac = a * c, bd = b * d, ad = a * d, bc = b * c;
-    x = ac - bd;
-    y = ad + bc;
-    if (__builtin_expect(__builtin_isnan(x) && __builtin_isnan(y), 0)) {
+    R ac = xmul(a, c), bd = xmul(b, d), ad = xmul(a, d), bc = xmul(b, c);
+    x = xsub(ac, bd);
+    y = xadd(ad, bc);
+    if (__builtin_expect(isnan_(x) && isnan_(y), 0)) {
         bool recalc = false;
         if (__builtin_isinf(a) || __builtin_isinf(b)) {
             a = __builtin_copysign(__builtin_isinf(a) ? (R)1 : (R)0, a);
             b = __builtin_copysign(__builtin_isinf(b) ? (R)1 : (R)0, b);
-            if (__builtin_isnan(c)) c = __builtin_copysign((R)0, c);
-            if (__builtin_isnan(d)) d = __builtin_copysign((R)0, d);
+            if (isnan_(c)) c = __builtin_copysign((R)0, c);
+            if (isnan_(d)) d = __builtin_copysign((R)0, d);
             recalc = true;
         }
         if (__builtin_isinf(c) || __builtin_isinf(d)) {
             c = __builtin_copysign(__builtin_isinf(c) ? (R)1 : (R)0, c);
             d = __builtin_copysign(__builtin_isinf(d) ? (R)1 : (R)0, d);
-            if (__builtin_isnan(a)) a = __builtin_copysign((R)0, a);
-            if (__builtin_isnan(b)) b = __builtin_copysign((R)0, b);
+            if (isnan_(a)) a = __builtin_copysign((R)0, a);
+            if (isnan_(b)) b = __builtin_copysign((R)0, b);
             recalc = true;
         }
         if (!recalc && (__builtin_isinf(ac) || __builtin_isinf(bd) || __builtin_isinf(ad) || __builtin_isinf(bc))) {
-            if (__builtin_isnan(a)) a = __builtin_copysign((R)0, a);
-            if (__builtin_isnan(b)) b = __builtin_copysign((R)0, b);
-            if (__builtin_isnan(c)) c = __builtin_copysign((R)0, c);
-            if (__builtin_isnan(d)) d = __builtin_copysign((R)0, d);
+            if (isnan_(a)) a = __builtin_copysign((R)0, a);
+            if (isnan_(b)) b = __builtin_copysign((R)0, b);
+            if (isnan_(c)) c = __builtin_copysign((R)0, c);
+            if (isnan_(d)) d = __builtin_copysign((R)0, d);
             recalc = true;
         }
         if (recalc) {
-            x = (R)__builtin_inf() * (a * c - b * d);
-            y = (R)__builtin_inf() * (a * d + b * c);
+            const R inf = (R)__builtin_inf();
+            x = xmul(inf, xsub(xmul(a, c), xmul(b, d)));
+            y = xmul(inf, xadd(xmul(a, d), xmul(b, c)));
         }
     }
 }
@@ -99,9 +141,9 @@ struct OpProd {
         typedef typename uns<T>::type U;
         return (T)(U)((U)a * (U)b);
     }
-    __device__ __forceinline__ f16 operator()(f16 a, f16 b) const { return a * b; }
-    __device__ __forceinline__ float operator()(float a, float b) const { return a * b; }
-    __device__ __forceinline__ double operator()(double a, double b) const { return a * b; }
+    __device__ __forceinline__ f16 operator()(f16 a, f16 b) const { return xmul(a, b); }
+    __device__ __forceinline__ float operator()(float a, float b) const { return xmul(a, b); }
+    __device__ __forceinline__ double operator()(double a, double b) const { return xmul(a, b); }
     __device__ __forceinline__ cf32 operator()(cf32 a, cf32 b) const {
         cf32 r; annexg_mul<float>(a.re, a.im, b.re, b.im, r.re, r.im); return r;
     }

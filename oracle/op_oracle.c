@@ -201,8 +201,45 @@ static uint16_t f2h(float f)    /* round to nearest even */
 #define ULOOP(ST, UT, F) do { ST *restrict a = (ST *) io; const ST *restrict b = (const ST *) in; \
         for (i = 0; i < len; i++) a[i] = (ST) (UT) F((UT) a[i], (UT) b[i]); } while (0)
 
-#define HLOOP_ARITH(F) do { uint16_t *a = (uint16_t *) io; const uint16_t *b = (const uint16_t *) in; \
-        for (i = 0; i < len; i++) a[i] = f2h(F(h2f(a[i]), h2f(b[i]))); } while (0)
+/* x86 SSE NaN rule (Intel SDM vol. 1, 4.8.3.5, Table 4-7): with a NaN operand
+ * the result is the FIRST source operand if it is a NaN, else the second,
+ * quieted.  The reference's loops put a[i] (inout) first -- gcc -O2:
+ * `movss a; addss b`, clang -O2: `addps b, a` (probed) -- so the result is
+ * quiet(a) if a is NaN, else quiet(b).  Made explicit here so the oracle does
+ * not depend on which operand order gcc picks for the helper calls below. */
+static float f_quiet(float x)
+{
+    uint32_t u;
+    memcpy(&u, &x, 4);
+    u |= 0x00400000u;
+    memcpy(&x, &u, 4);
+    return x;
+}
+
+static double d_quiet(double x)
+{
+    uint64_t u;
+    memcpy(&u, &x, 8);
+    u |= 0x0008000000000000ull;
+    memcpy(&x, &u, 8);
+    return x;
+}
+
+#define NANRULE(Q, F) ((a[i] != a[i]) ? Q(a[i]) : (b[i] != b[i]) ? Q(b[i]) : F(a[i], b[i]))
+#define FLOOP(T, Q, F) do { T *restrict a = (T *) io; const T *restrict b = (const T *) in; \
+        for (i = 0; i < len; i++) a[i] = NANRULE(Q, F); } while (0)
+
+static float h_arith(float x, float y, int prod)
+{
+    if (x != x)
+        return f_quiet(x);
+    if (y != y)
+        return f_quiet(y);
+    return prod ? x * y : x + y;
+}
+
+#define HLOOP_ARITH(PROD) do { uint16_t *a = (uint16_t *) io; const uint16_t *b = (const uint16_t *) in; \
+        for (i = 0; i < len; i++) a[i] = f2h(h_arith(h2f(a[i]), h2f(b[i]), PROD)); } while (0)
 /* MPL_MAX on _Float16: compare the promoted values, select the original bits */
 #define HLOOP_SEL(CMP) do { uint16_t *a = (uint16_t *) io; const uint16_t *b = (const uint16_t *) in; \
         for (i = 0; i < len; i++) a[i] = (h2f(a[i]) CMP h2f(b[i])) ? a[i] : b[i]; } while (0)
@@ -232,9 +269,9 @@ static int apply(int opidx, int kind, const void *in, void *io, int len)
         case K_U32: LOOP(uint32_t, LSUM); return 0;
         case K_I64: ULOOP(int64_t, uint64_t, LSUM); return 0;
         case K_U64: LOOP(uint64_t, LSUM); return 0;
-        case K_F16: HLOOP_ARITH(LSUM); return 0;
-        case K_F32: LOOP(float, LSUM); return 0;
-        case K_F64: LOOP(double, LSUM); return 0;
+        case K_F16: HLOOP_ARITH(0); return 0;
+        case K_F32: FLOOP(float, f_quiet, LSUM); return 0;
+        case K_F64: FLOOP(double, d_quiet, LSUM); return 0;
         case K_CF32: LOOP(float _Complex, LSUM); return 0;
         case K_CF64: LOOP(double _Complex, LSUM); return 0;
         }
@@ -249,9 +286,9 @@ static int apply(int opidx, int kind, const void *in, void *io, int len)
         case K_U32: LOOP(uint32_t, LPROD); return 0;
         case K_I64: ULOOP(int64_t, uint64_t, LPROD); return 0;
         case K_U64: LOOP(uint64_t, LPROD); return 0;
-        case K_F16: HLOOP_ARITH(LPROD); return 0;
-        case K_F32: LOOP(float, LPROD); return 0;
-        case K_F64: LOOP(double, LPROD); return 0;
+        case K_F16: HLOOP_ARITH(1); return 0;
+        case K_F32: FLOOP(float, f_quiet, LPROD); return 0;
+        case K_F64: FLOOP(double, d_quiet, LPROD); return 0;
         case K_CF32: LOOP(float _Complex, LPROD); return 0;
         case K_CF64: LOOP(double _Complex, LPROD); return 0;
         }

@@ -230,3 +230,57 @@ def test_config2_64mib_repeat_idempotence(mpi, cuda):
     for _ in range(2):
         assert mpi.reduce_local(y.data_ptr(), x.data_ptr(), n, mpi.MPI_FLOAT, mpi.MPI_SUM) == 0
     assert torch.equal(x.view(torch.int32), ref.view(torch.int32))
+
+
+def _pairs(specials, ut):
+    v = np.array(specials, dtype=ut)
+    return np.repeat(v, len(v)), np.tile(v, len(v))
+
+
+@pytest.mark.parametrize("op", ["MPI_SUM", "MPI_PROD", "MPI_MAX", "MPI_MIN", "MPI_LXOR"])
+@pytest.mark.parametrize("t", ["MPI_FLOAT", "MPI_DOUBLE", "MPIX_C_FLOAT16"])
+def test_nan_inf_zero_pairs(mpi, orc, cuda, op, t):
+    """Every pairing of NaN (quiet/signalling, both signs, payloads), +-inf, +-0,
+    denormals and extremes: NaN payload propagation and the default NaN of
+    invalid operations (inf - inf, 0 * inf) must match the reference bit for bit."""
+    ut, sp = {"MPI_FLOAT": (np.uint32, T.F32_SPECIALS), "MPI_DOUBLE": (np.uint64, T.F64_SPECIALS),
+              "MPIX_C_FLOAT16": (np.uint16, T.F16_SPECIALS)}[t]
+    a, b = _pairs(sp, ut)
+    want = a.copy()
+    assert orc.reduce_local(b.copy(), want, len(a), mpi.DATATYPES[t], mpi.OPS[op]) == 0
+    tio, pio = dev(cuda, a.view(np.uint8))
+    tin, pin = dev(cuda, b.view(np.uint8))
+    assert mpi.reduce_local(pin, pio, len(a), mpi.DATATYPES[t], mpi.OPS[op]) == 0
+    got = back(tio, 0, a.nbytes)
+    if not np.array_equal(got, want.view(np.uint8)):
+        pytest.fail(f"{op} {t}:\n" + explain(got, want.view(np.uint8), a.view(np.uint8), b.view(np.uint8),
+                                             np.dtype(ut).itemsize, limit=40))
+
+
+@pytest.mark.parametrize("op", ["MPI_SUM", "MPI_PROD"])
+@pytest.mark.parametrize("t", ["MPI_C_FLOAT_COMPLEX", "MPI_C_DOUBLE_COMPLEX"])
+def test_complex_special_pairs(mpi, orc, cuda, op, t):
+    """C99 Annex G complex multiply (NaN recovery branch) and component sums over
+    special real/imaginary parts."""
+    ft = np.float32 if t == "MPI_C_FLOAT_COMPLEX" else np.float64
+    vals = np.array([np.nan, np.nan, np.nan, np.inf, -np.inf, 0.0, -0.0, 1.5, -2.0,
+                     3e38 if ft == np.float32 else 1e308], dtype=ft)
+    ut = np.uint32 if ft == np.float32 else np.uint64
+    bits = vals.view(ut)          # NaNs with distinct payloads / sign
+    bits[1] = 0xFFC00000 if ft == np.float32 else 0xFFF8000000000000
+    bits[2] = 0x7FC00123 if ft == np.float32 else 0x7FF8000000000123
+    z = (vals[:, None] + 0j * vals[None, :]).astype(np.complex64 if ft == np.float32 else np.complex128)
+    z.real = np.repeat(vals, len(vals)).reshape(len(vals), len(vals))
+    z.imag = np.tile(vals, len(vals)).reshape(len(vals), len(vals))
+    z = z.reshape(-1)
+    a = np.repeat(z, len(z))
+    b = np.tile(z, len(z))
+    want = a.copy()
+    assert orc.reduce_local(b.copy(), want, len(a), mpi.DATATYPES[t], mpi.OPS[op]) == 0
+    tio, pio = dev(cuda, a.view(np.uint8))
+    tin, pin = dev(cuda, b.view(np.uint8))
+    assert mpi.reduce_local(pin, pio, len(a), mpi.DATATYPES[t], mpi.OPS[op]) == 0
+    got = back(tio, 0, a.nbytes)
+    if not np.array_equal(got, want.view(np.uint8)):
+        pytest.fail(f"{op} {t}:\n" + explain(got, want.view(np.uint8), a.view(np.uint8), b.view(np.uint8),
+                                             a.itemsize, limit=30))
