@@ -46,6 +46,26 @@ def explain(got, want, a, b, esz, limit=6):
     return "\n".join(lines)
 
 
+def same(got: np.ndarray, want: np.ndarray, t: str) -> bool:
+    """Bit-exact, except the NaN payload/sign of C _Complex results: C leaves the
+    payload of a NaN result to codegen, and gcc -O2 orders the complex
+    component operations differently depending on the surrounding switch
+    (probed: standalone `a[i] + b[i]` puts a.im first, the same loop inside the
+    op switch puts b.im first), so it is not a property of the reference.
+    Non-NaN complex components (infinities of the Annex G recovery included)
+    stay bit-exact; real types are bit-exact including NaN payloads."""
+    if np.array_equal(got, want):
+        return True
+    if t not in T.CPLX:
+        return False
+    ft = np.float32 if t == "MPI_C_FLOAT_COMPLEX" else np.float64
+    ut = np.uint32 if ft == np.float32 else np.uint64
+    g = got.view(ft)
+    w = want.view(ft)
+    ok = (got.view(ut) == want.view(ut)) | (np.isnan(g) & np.isnan(w))
+    return bool(ok.all())
+
+
 def run_pair(mpi, orc, torch, op, t, n, seed, off_in=0, off_io=0):
     rng = np.random.default_rng(seed)
     a = T.to_bytes(T.gen(t, n, rng, op))          # inout
@@ -58,7 +78,7 @@ def run_pair(mpi, orc, torch, op, t, n, seed, off_in=0, off_io=0):
     got = back(tio, off_io, a.size)
     assert rc == rc_o, (op, t, rc, rc_o)
     assert np.array_equal(back(tin, off_in, b.size), b), "inbuf modified"
-    if not np.array_equal(got, want):
+    if not same(got, want, t):
         pytest.fail(f"{op} {t} n={n} off=({off_in},{off_io}):\n" + explain(got, want, a, b, T.elem_size(t)))
 
 
@@ -281,6 +301,9 @@ def test_complex_special_pairs(mpi, orc, cuda, op, t):
     tin, pin = dev(cuda, b.view(np.uint8))
     assert mpi.reduce_local(pin, pio, len(a), mpi.DATATYPES[t], mpi.OPS[op]) == 0
     got = back(tio, 0, a.nbytes)
-    if not np.array_equal(got, want.view(np.uint8)):
+    if not same(got, want.view(np.uint8), t):
         pytest.fail(f"{op} {t}:\n" + explain(got, want.view(np.uint8), a.view(np.uint8), b.view(np.uint8),
                                              a.itemsize, limit=30))
+    # the non-NaN part really is exercised: infinities from the Annex G recovery
+    if op == "MPI_PROD":
+        assert np.isinf(got.view(ft)).sum() > 100
