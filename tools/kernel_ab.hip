@@ -29,6 +29,66 @@ struct OpSumPlain {
     __device__ __forceinline__ float operator()(float a, float b) const { return a + b; }
 };
 
+// ---- experimental shapes (not the product) --------------------------------
+__device__ __forceinline__ void ld_tile(const char *in, char *io, uint64_t vbytes, uint64_t t, u32x4 *a, u32x4 *b) {
+    const uint64_t base = t * kTileBytes;
+    const uint64_t left = vbytes - base;
+    const int nrec = (int)(left < kTileBytes ? left : kTileBytes);
+    __amdgpu_buffer_rsrc_t rin = __builtin_amdgcn_make_buffer_rsrc((void *)(in + base), 0, nrec, 0x00020000);
+    __amdgpu_buffer_rsrc_t rio = __builtin_amdgcn_make_buffer_rsrc((void *)(io + base), 0, nrec, 0x00020000);
+#pragma unroll
+    for (int u = 0; u < kVecPerLane; ++u) {
+        const int off = (u * kThreads + (int)threadIdx.x) * 16;
+        a[u] = __builtin_amdgcn_raw_buffer_load_b128(rio, off, 0, kCachePolicyNT);
+        b[u] = __builtin_amdgcn_raw_buffer_load_b128(rin, off, 0, kCachePolicyNT);
+    }
+}
+__device__ __forceinline__ void st_tile(char *io, uint64_t vbytes, uint64_t t, const u32x4 *a, const u32x4 *b) {
+    const uint64_t base = t * kTileBytes;
+    const uint64_t left = vbytes - base;
+    const int nrec = (int)(left < kTileBytes ? left : kTileBytes);
+    __amdgpu_buffer_rsrc_t rio = __builtin_amdgcn_make_buffer_rsrc((void *)(io + base), 0, nrec, 0x00020000);
+#pragma unroll
+    for (int u = 0; u < kVecPerLane; ++u) {
+        const int off = (u * kThreads + (int)threadIdx.x) * 16;
+        __builtin_amdgcn_raw_buffer_store_b128(combine16<OpSum, float>(a[u], b[u]), rio, off, 0, kCachePolicyNT);
+    }
+}
+// persistent + register double buffer: next tile's loads in flight while storing this one
+__global__ __launch_bounds__(256) void k_pipe(const char *in, char *io, uint64_t vbytes, uint64_t ntiles) {
+    uint64_t t = blockIdx.x;
+    if (t >= ntiles) return;
+    u32x4 a[kVecPerLane], b[kVecPerLane], a2[kVecPerLane], b2[kVecPerLane];
+    ld_tile(in, io, vbytes, t, a, b);
+    for (; t < ntiles; t += gridDim.x) {
+        const uint64_t tn = t + gridDim.x;
+        if (tn < ntiles) ld_tile(in, io, vbytes, tn, a2, b2);
+        st_tile(io, vbytes, t, a, b);
+#pragma unroll
+        for (int u = 0; u < kVecPerLane; ++u) { a[u] = a2[u]; b[u] = b2[u]; }
+    }
+}
+template <int GRID>
+hipError_t launch_pipe(const void *in, void *io, uint64_t count, hipStream_t s) {
+    uint64_t vbytes = count * 4, ntiles = (vbytes + kTileBytes - 1) / kTileBytes;
+    hipLaunchKernelGGL(k_pipe, dim3(GRID), dim3(256), 0, s, (const char *)in, (char *)io, vbytes, ntiles);
+    return hipGetLastError();
+}
+// two tiles per workgroup, second tile's loads issued before the first tile's stores
+__global__ __launch_bounds__(256) void k_two(const char *in, char *io, uint64_t vbytes, uint64_t ntiles) {
+    uint64_t t = 2 * (uint64_t)blockIdx.x;
+    u32x4 a[kVecPerLane], b[kVecPerLane], a2[kVecPerLane], b2[kVecPerLane];
+    ld_tile(in, io, vbytes, t, a, b);
+    if (t + 1 < ntiles) ld_tile(in, io, vbytes, t + 1, a2, b2);
+    st_tile(io, vbytes, t, a, b);
+    if (t + 1 < ntiles) st_tile(io, vbytes, t + 1, a2, b2);
+}
+hipError_t launch_two(const void *in, void *io, uint64_t count, hipStream_t s) {
+    uint64_t vbytes = count * 4, ntiles = (vbytes + kTileBytes - 1) / kTileBytes;
+    hipLaunchKernelGGL(k_two, dim3((ntiles + 1) / 2), dim3(256), 0, s, (const char *)in, (char *)io, vbytes, ntiles);
+    return hipGetLastError();
+}
+
 struct Var {
     std::string name;
     size_t esz;
@@ -52,31 +112,13 @@ int main(int argc, char **argv) {
         CK(hipMemcpy(io[s], h.data(), bytes, hipMemcpyHostToDevice));
     }
     std::vector<Var> vs = {
-        {"SUM fp32 (x86 NaN rule)", 4, &launch_reduce<OpSum, float>, {}},
-        {"SUM fp32 (plain add)", 4, &launch_reduce<OpSumPlain, float>, {}},
-        {"SUM fp64", 8, &launch_reduce<OpSum, double>, {}},
-        {"SUM int32", 4, &launch_reduce<OpSum, int32_t>, {}},
-        {"SUM int64", 8, &launch_reduce<OpSum, int64_t>, {}},
-        {"MAX fp32", 4, &launch_reduce<OpMax, float>, {}},
-        {"MAX fp64", 8, &launch_reduce<OpMax, double>, {}},
-        {"MAX int32", 4, &launch_reduce<OpMax, int32_t>, {}},
-        {"MAX int64", 8, &launch_reduce<OpMax, int64_t>, {}},
-        {"MIN fp32", 4, &launch_reduce<OpMin, float>, {}},
-        {"MIN fp64", 8, &launch_reduce<OpMin, double>, {}},
-        {"MIN int32", 4, &launch_reduce<OpMin, int32_t>, {}},
-        {"MIN int64", 8, &launch_reduce<OpMin, int64_t>, {}},
-        {"PROD fp32", 4, &launch_reduce<OpProd, float>, {}},
-        {"PROD fp64", 8, &launch_reduce<OpProd, double>, {}},
-        {"PROD int32", 4, &launch_reduce<OpProd, int32_t>, {}},
-        {"PROD int64", 8, &launch_reduce<OpProd, int64_t>, {}},
-        {"SUM fp16", 2, &launch_reduce<OpSum, f16>, {}},
-        {"SUM cf32", 8, &launch_reduce<OpSum, cf32>, {}},
-        {"PROD cf32", 8, &launch_reduce<OpProd, cf32>, {}},
-        {"PROD cf64", 16, &launch_reduce<OpProd, cf64>, {}},
-        {"BXOR uint8", 1, &launch_reduce<OpBxor, uint8_t>, {}},
-        {"LXOR fp32", 4, &launch_reduce<OpLxor, float>, {}},
-        {"MAXLOC 2int", 8, &launch_reduce<OpMaxloc, p2int>, {}},
-        {"MAXLOC double_int", 16, &launch_reduce<OpMaxloc, pdoubleint>, {}},
+        {"SUM fp32 product", 4, &launch_reduce<OpSum, float>, {}},
+        {"SUM fp32 plain add", 4, &launch_reduce<OpSumPlain, float>, {}},
+        {"SUM fp32 pipe grid 1024", 4, &launch_pipe<1024>, {}},
+        {"SUM fp32 pipe grid 2048", 4, &launch_pipe<2048>, {}},
+        {"SUM fp32 pipe grid 4096", 4, &launch_pipe<4096>, {}},
+        {"SUM fp32 two tiles/WG", 4, &launch_two, {}},
+        {"SUM fp32 product (again)", 4, &launch_reduce<OpSum, float>, {}},
     };
     hipStream_t st;
     CK(hipStreamCreate(&st));
