@@ -208,6 +208,21 @@ int MPI_Error_string(int errorcode, char *string, int *resultlen);
  * as MPI_Reduce_local; user ops give MPI_ERR_OP (they run on the host). */
 int MPIX_Reduce_local_stream(const void *inbuf, void *inoutbuf, int count, MPI_Datatype datatype,
                              MPI_Op op, void *hip_stream);
+/* Multi-operand local reduction: outbuf = fold of n device buffers in ONE pass
+ * over HBM, in the association a reduction schedule would produce by calling
+ * MPIR_Reduce_local step by step (bit-identical to doing exactly that):
+ *   MPIX_ORDER_TREE  (n = 1, 2, 4, 8): ((b0+b1)+(b2+b3))+((b4+b5)+(b6+b7)) --
+ *       recursive halving, reduce_intra_reduce_scatter_gather.c:186-249;
+ *   MPIX_ORDER_CHAIN (1 <= n <= 64): ((b0+b1)+b2)+... -- pairwise,
+ *       reduce_scatter_block_intra_pairwise.c:97-134.
+ * In each step the left operand is the step's inoutbuf.  outbuf may alias
+ * inbufs[0].  hip_stream NULL: synchronous on the library stream; otherwise
+ * enqueued on that stream without waiting.  Builtin ops and basic types with
+ * the same validation as MPI_Reduce_local. */
+#define MPIX_ORDER_TREE  0
+#define MPIX_ORDER_CHAIN 1
+int MPIX_Reduce_local_multi(const void *const *inbufs, int n, void *outbuf, int count,
+                            MPI_Datatype datatype, MPI_Op op, int order, void *hip_stream);
 int MPIX_Reduce_local_set_errhandler(MPI_Errhandler errhandler);
 int MPIX_Reduce_local_get_errhandler(MPI_Errhandler * errhandler);
 

@@ -65,6 +65,19 @@ enum MPIR_Hip_elem {
 int MPIR_Hip_reduce(const void *inbuf, void *inoutbuf, uint64_t count, int op, int elem,
                     void *hip_stream, int sync);
 
+/* Multi-operand combine: outbuf = fold(inbufs[0..n-1]) in one pass, in the
+ * association of a reduction schedule (the schedule's MPIR_Reduce_local steps
+ * fused; left operand = the step's inoutbuf):
+ *   MPIR_HIP_ORDER_TREE  (n = 1, 2, 4, 8): ((y0+y1)+(y2+y3))+((y4+y5)+(y6+y7)),
+ *       the recursive-halving order of reduce_intra_reduce_scatter_gather.c;
+ *   MPIR_HIP_ORDER_CHAIN (1 <= n <= 64): ((y0+y1)+y2)+..., the pairwise order
+ *       of reduce_scatter_block_intra_pairwise.c.
+ * All buffers device-resident on one device; outbuf may alias inbufs[0]. */
+#define MPIR_HIP_ORDER_TREE  0
+#define MPIR_HIP_ORDER_CHAIN 1
+int MPIR_Hip_combine(const void *const *inbufs, int n, void *outbuf, uint64_t count, int op, int elem,
+                     int order, void *hip_stream, int sync);
+
 /* byte size of an element class (0 if unknown) */
 size_t MPIR_Hip_elem_size(int elem);
 /* 1 if a kernel exists for (op, elem) */

@@ -68,6 +68,36 @@ struct TableInit {
     }
 } g_table_init;
 
+// ---- multi-operand (fused schedule) combines: [op][elem][order][P = 2, 4, 8]
+typedef hipError_t (*multi_fn)(const void *const *, void *, uint64_t, hipStream_t);
+multi_fn g_multi[MPIR_HIP_NOPS][MPIR_HIP_NELEMS][2][3];
+
+template <class Op, class T>
+void reg_multi(int op, int elem) {
+    g_multi[op][elem][0][0] = &launch_combine_p<Op, T, 2, true>;
+    g_multi[op][elem][0][1] = &launch_combine_p<Op, T, 4, true>;
+    g_multi[op][elem][0][2] = &launch_combine_p<Op, T, 8, true>;
+    g_multi[op][elem][1][0] = &launch_combine_p<Op, T, 2, false>;
+    g_multi[op][elem][1][1] = &launch_combine_p<Op, T, 4, false>;
+    g_multi[op][elem][1][2] = &launch_combine_p<Op, T, 8, false>;
+}
+
+struct MultiInit {
+    MultiInit() {
+        memset(g_multi, 0, sizeof(g_multi));
+        // the ops the reduction collectives are built on (configs 4-5): SUM/PROD/MAX/MIN
+        // over integers and reals (+ complex SUM/PROD).  Other (op, type) pairs run
+        // the schedule step by step through MPIR_Hip_reduce.
+#define X(E, T) reg_multi<OpSum, T>(MPIR_HIP_OP_SUM, E); reg_multi<OpProd, T>(MPIR_HIP_OP_PROD, E); \
+                reg_multi<OpMax, T>(MPIR_HIP_OP_MAX, E); reg_multi<OpMin, T>(MPIR_HIP_OP_MIN, E);
+        X(MPIR_HIP_I32, int32_t) X(MPIR_HIP_U32, uint32_t) X(MPIR_HIP_I64, int64_t) X(MPIR_HIP_U64, uint64_t)
+        X(MPIR_HIP_F16, f16) X(MPIR_HIP_F32, float) X(MPIR_HIP_F64, double)
+#undef X
+        reg_multi<OpSum, cf32>(MPIR_HIP_OP_SUM, MPIR_HIP_CF32);
+        reg_multi<OpSum, cf64>(MPIR_HIP_OP_SUM, MPIR_HIP_CF64);
+    }
+} g_multi_init;
+
 const size_t g_elem_size[MPIR_HIP_NELEMS] = {
     0, 1, 1, 2, 2, 4, 4, 8, 8, 2, 4, 8, 8, 16, 8, 8, 16, 8, 16,
 };
@@ -112,6 +142,8 @@ int get_stream(int dev, int slot, hipStream_t *out) {
 int get_scratch(int dev, size_t bytes, char **out) {
     DevCtx &d = t_ctx.dev[dev];
     if (d.scratch_bytes < bytes) {
+        // stream-ordered users of the old scratch may still be in flight
+        if (d.scratch) HIPCHK(hipDeviceSynchronize());
         if (d.scratch) HIPCHK(hipFree(d.scratch));
         d.scratch = nullptr;
         d.scratch_bytes = 0;
@@ -221,6 +253,87 @@ int MPIR_Hip_memcpy(void *dst, const void *src, size_t bytes) {
     if (!bytes) return MPIR_HIP_OK;
     HIPCHK(hipMemcpy(dst, src, bytes, hipMemcpyDefault));
     return MPIR_HIP_OK;
+}
+
+int MPIR_Hip_combine(const void *const *inbufs, int n, void *outbuf, uint64_t count, int op, int elem,
+                     int order, void *hip_stream, int sync) {
+    t_ctx.err[0] = 0;
+    if (n < 1 || n > 64 || (order != MPIR_HIP_ORDER_TREE && order != MPIR_HIP_ORDER_CHAIN)) return MPIR_HIP_ENOKERNEL;
+    if (op <= 0 || op >= MPIR_HIP_NOPS || elem <= 0 || elem >= MPIR_HIP_NELEMS) return MPIR_HIP_ENOKERNEL;
+    if (order == MPIR_HIP_ORDER_TREE && (n & (n - 1))) return MPIR_HIP_ENOKERNEL;
+    const size_t esz = g_elem_size[elem];
+    int dev = -1;
+    if (classify(outbuf, &dev) != LOC_DEVICE) return MPIR_HIP_EBUFFER;
+    for (int j = 0; j < n; ++j) {
+        int d = -1;
+        if (classify(inbufs[j], &d) != LOC_DEVICE || d != dev) return MPIR_HIP_EBUFFER;
+    }
+    int cur = 0;
+    HIPCHK(hipGetDevice(&cur));
+    if (cur != dev) HIPCHK(hipSetDevice(dev));
+    hipStream_t s = (hipStream_t)hip_stream;
+    int rc = MPIR_HIP_OK;
+    if (!s) rc = get_stream(dev, 0, &s);
+    hipError_t e = hipSuccess;
+    if (rc == MPIR_HIP_OK && count > 0) {
+        const bool fused = g_multi[op][elem][0][0] != nullptr;
+        if (n == 1) {
+            if (outbuf != inbufs[0]) e = hipMemcpyAsync(outbuf, inbufs[0], count * esz, hipMemcpyDeviceToDevice, s);
+        } else if (order == MPIR_HIP_ORDER_TREE) {
+            if (fused && n <= 8) {
+                e = g_multi[op][elem][0][n == 2 ? 0 : (n == 4 ? 1 : 2)](inbufs, outbuf, count, s);
+            } else if (!g_table[op][elem].fn) {
+                rc = MPIR_HIP_ENOKERNEL;
+            } else {
+                // Level by level with the single-operand kernel, same association:
+                // v_j = v_j (+) v_{j+step} (left operand = v_j).  v_0 lives in
+                // outbuf, v_j (j > 0 even) in device scratch.
+                const uint64_t bytes = count * esz, slot = (bytes + 255) & ~(uint64_t)255;
+                const uint64_t unit = (op == MPIR_HIP_OP_REPLACE) ? 1 : esz;
+                char *scr = nullptr;
+                if (n > 2) rc = get_scratch(dev, (size_t)(n / 2 - 1) * slot, &scr);
+                void *v[64];
+                for (int j = 0; j < n && rc == MPIR_HIP_OK; ++j) v[j] = const_cast<void *>(inbufs[j]);
+                for (int step = 1; step < n && rc == MPIR_HIP_OK && e == hipSuccess; step *= 2) {
+                    for (int j = 0; j < n && e == hipSuccess; j += 2 * step) {
+                        if (step == 1) {   // first level: copy y_j into its accumulator slot
+                            void *dst = j == 0 ? outbuf : scr + (uint64_t)(j / 2 - 1) * slot;
+                            if (dst != v[j]) e = hipMemcpyAsync(dst, v[j], bytes, hipMemcpyDeviceToDevice, s);
+                            v[j] = dst;
+                        }
+                        if (e == hipSuccess) e = g_table[op][elem].fn(v[j + step], v[j], bytes / unit, s);
+                    }
+                }
+            }
+        } else {
+            // CHAIN: acc = y0; fold y1..y_{n-1} in order.  Greedy chunks of
+            // P = 8/4/2 operands, each chunk's first operand the running acc.
+            const void *acc = inbufs[0];
+            int i = 1;
+            while (e == hipSuccess && rc == MPIR_HIP_OK && i < n) {
+                const int left = n - i;
+                if (fused) {
+                    const int P = left >= 7 ? 8 : (left >= 3 ? 4 : 2);
+                    const void *ops[8];
+                    ops[0] = acc;
+                    for (int j = 1; j < P; ++j) ops[j] = inbufs[i + j - 1];
+                    e = g_multi[op][elem][1][P == 2 ? 0 : (P == 4 ? 1 : 2)](ops, outbuf, count, s);
+                    i += P - 1;
+                } else {
+                    if (acc != outbuf) e = hipMemcpyAsync(outbuf, acc, count * esz, hipMemcpyDeviceToDevice, s);
+                    const uint64_t unit = (op == MPIR_HIP_OP_REPLACE) ? 1 : esz;
+                    if (e == hipSuccess) e = g_table[op][elem].fn ? g_table[op][elem].fn(inbufs[i], outbuf, count * esz / unit, s)
+                                                                 : hipErrorInvalidValue;
+                    i += 1;
+                }
+                acc = outbuf;
+            }
+        }
+        if (e != hipSuccess) rc = set_err(e, "combine launch");
+        if (rc == MPIR_HIP_OK && sync) rc = wait_stream(dev, s);
+    }
+    if (cur != dev) (void)hipSetDevice(cur);
+    return rc;
 }
 
 int MPIR_Hip_reduce(const void *inbuf, void *inoutbuf, uint64_t count, int op, int elem, void *hip_stream,

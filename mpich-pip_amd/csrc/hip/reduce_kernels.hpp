@@ -154,4 +154,148 @@ hipError_t launch_reduce(const void *in_, void *io_, uint64_t count, hipStream_t
     return hipGetLastError();
 }
 
+
+// ============================================================================
+// Multi-operand combines: the log2(p) / (p-1) MPIR_Reduce_local steps of a
+// reduction schedule fused into ONE pass over HBM, in the schedule's exact
+// association and operand order (so results are bit-identical to running the
+// reference schedule step by step).
+//
+//   TREE  (recursive halving: reduce_intra_reduce_scatter_gather.c:186-249,
+//          allreduce_intra_reduce_scatter_allgather.c:150-215):
+//          v_j = y_j; for l = 0..L-1: v_j = v_j (+) v_{j + 2^l}, j % 2^(l+1) == 0
+//          i.e. ((y0+y1)+(y2+y3))+((y4+y5)+(y6+y7)), left operand = inout.
+//          The caller orders y_j = contribution of newrank (owner ^ j).
+//   CHAIN (pairwise: reduce_scatter_block_intra_pairwise.c:97-134):
+//          acc = y0; acc = acc (+) y1; ...; acc = acc (+) y_{P-1}.
+//
+// One workgroup reads P x TILE bytes and writes TILE bytes; the lane keeps
+// P 16-byte loads in flight (P x 1 KiB per wave-instruction group).
+// ============================================================================
+constexpr int kMaxOperands = 16;
+
+struct MultiArgs {
+    const char *in[kMaxOperands];   // 16 B-aligned vector regions, same alignment as out
+    char *out;
+    uint64_t vbytes;                // multiple of 16
+    uint32_t nhead, ntail;          // scalar elements before / after the vector region
+    int64_t head_off, tail_off;     // byte offsets of head / tail from the region starts
+};
+
+template <class Op, class T, int P, bool TREE>
+__device__ __forceinline__ void fold_elems(T (&v)[P]) {
+    Op op;
+    if constexpr (TREE) {
+#pragma unroll
+        for (int step = 1; step < P; step *= 2)
+#pragma unroll
+            for (int j = 0; j < P; j += 2 * step) v[j] = op(v[j], v[j + step]);
+    } else {
+#pragma unroll
+        for (int j = 1; j < P; ++j) v[0] = op(v[0], v[j]);
+    }
+}
+
+template <class Op, class T, int P, bool TREE, int U>
+__global__ __launch_bounds__(kThreads) void k_combine_multi(MultiArgs a) {
+    constexpr uint32_t tile = kThreads * U * 16;
+    const uint64_t base = (uint64_t)blockIdx.x * tile;
+    if (base < a.vbytes) {
+        const uint64_t left = a.vbytes - base;
+        const int nrec = (int)(left < tile ? left : tile);
+        u32x4 x[P][U];
+#pragma unroll
+        for (int j = 0; j < P; ++j) {
+            __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void *)(a.in[j] + base), 0, nrec, 0x00020000);
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                x[j][u] = __builtin_amdgcn_raw_buffer_load_b128(r, (u * kThreads + (int)threadIdx.x) * 16, 0, kCachePolicyNT);
+        }
+        __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc((void *)(a.out + base), 0, nrec, 0x00020000);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            Pack16<T> pk[P];
+#pragma unroll
+            for (int j = 0; j < P; ++j) pk[j] = __builtin_bit_cast(Pack16<T>, x[j][u]);
+            Pack16<T> res;
+#pragma unroll
+            for (int k = 0; k < (int)(16 / sizeof(T)); ++k) {
+                T v[P];
+#pragma unroll
+                for (int j = 0; j < P; ++j) v[j] = pk[j].e[k];
+                fold_elems<Op, T, P, TREE>(v);
+                res.e[k] = v[0];
+            }
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, res), ro,
+                                                   (u * kThreads + (int)threadIdx.x) * 16, 0, kCachePolicyNT);
+        }
+    }
+    if (blockIdx.x == 0) {
+        const unsigned t = threadIdx.x;
+        int64_t off = 0;
+        bool act = false;
+        if (t < a.nhead) { off = a.head_off + (int64_t)(t * sizeof(T)); act = true; }
+        else if (t >= 64 && t - 64 < a.ntail) { off = a.tail_off + (int64_t)((t - 64) * sizeof(T)); act = true; }
+        if (act) {
+            T v[P];
+#pragma unroll
+            for (int j = 0; j < P; ++j) v[j] = *reinterpret_cast<const T *>(a.in[j] + off);
+            fold_elems<Op, T, P, TREE>(v);
+            *reinterpret_cast<T *>(a.out + off) = v[0];
+        }
+    }
+}
+
+// Misaligned operands: element-granular grid-stride fallback.
+template <class Op, class T, int P, bool TREE>
+__global__ __launch_bounds__(kThreads) void k_combine_multi_elems(MultiArgs a, uint64_t n) {
+    const uint64_t stride = (uint64_t)gridDim.x * kThreads;
+    for (uint64_t i = (uint64_t)blockIdx.x * kThreads + threadIdx.x; i < n; i += stride) {
+        T v[P];
+#pragma unroll
+        for (int j = 0; j < P; ++j) __builtin_memcpy(&v[j], a.in[j] + i * sizeof(T), sizeof(T));
+        fold_elems<Op, T, P, TREE>(v);
+        __builtin_memcpy(a.out + i * sizeof(T), &v[0], sizeof(T));
+    }
+}
+
+template <class Op, class T, int P, bool TREE>
+hipError_t launch_combine_p(const void *const *ins, void *out_, uint64_t count, hipStream_t s) {
+    constexpr int U = P >= 8 ? 1 : (P >= 4 ? 2 : 4);
+    constexpr uint32_t tile = kThreads * U * 16;
+    char *out = static_cast<char *>(out_);
+    const uintptr_t ao = reinterpret_cast<uintptr_t>(out);
+    const uint64_t nbytes = count * sizeof(T);
+    bool vec_ok = (ao % alignof(T) == 0) && (((16 - (ao & 15)) & 15) % sizeof(T) == 0);
+    for (int j = 0; j < P; ++j) {
+        const uintptr_t ai = reinterpret_cast<uintptr_t>(ins[j]);
+        vec_ok = vec_ok && (ai % alignof(T) == 0) && (((ai ^ ao) & 15) == 0);
+    }
+    MultiArgs a;
+    for (int j = 0; j < kMaxOperands; ++j) a.in[j] = j < P ? static_cast<const char *>(ins[j]) : nullptr;
+    if (vec_ok) {
+        uint64_t head = (16 - (ao & 15)) & 15;
+        if (head > nbytes) head = nbytes;
+        const uint64_t rest = nbytes - head, vbytes = rest & ~(uint64_t)15;
+        for (int j = 0; j < P; ++j) a.in[j] += head;
+        a.out = out + head;
+        a.vbytes = vbytes;
+        a.nhead = (uint32_t)(head / sizeof(T));
+        a.head_off = -(int64_t)head;                // head elements sit before the region start
+        a.ntail = (uint32_t)((rest - vbytes) / sizeof(T));
+        a.tail_off = (int64_t)vbytes;
+        uint64_t grid = (vbytes + tile - 1) / tile;
+        if (grid == 0) grid = 1;
+        hipLaunchKernelGGL((k_combine_multi<Op, T, P, TREE, U>), dim3((unsigned)grid), dim3(kThreads), 0, s, a);
+    } else {
+        a.out = out;
+        a.vbytes = 0;
+        uint64_t grid = (count + kThreads - 1) / kThreads;
+        if (grid > 4096) grid = 4096;
+        if (grid == 0) grid = 1;
+        hipLaunchKernelGGL((k_combine_multi_elems<Op, T, P, TREE>), dim3((unsigned)grid), dim3(kThreads), 0, s, a, count);
+    }
+    return hipGetLastError();
+}
+
 }  // namespace mpir_hip

@@ -350,6 +350,51 @@ int MPIX_Reduce_local_stream(const void *inbuf, void *inoutbuf, int count, MPI_D
     return MPI_SUCCESS;
 }
 
+/* ---- MPIX_Reduce_local_multi: fused schedule steps (see the header) ---- */
+int MPIX_Reduce_local_multi(const void *const *inbufs, int n, void *outbuf, int count,
+                            MPI_Datatype datatype, MPI_Op op, int order, void *hip_stream)
+{
+    static const char *fc = "MPIX_Reduce_local_multi";
+    int mpi_errno, opidx, elem, rc, j;
+    if (n < 1 || n > 64 || !inbufs || (order != MPIX_ORDER_TREE && order != MPIX_ORDER_CHAIN)) {
+        MPIR_Err_set_detail("invalid operand count or order");
+        return err_return(fc, MPI_ERR_ARG);
+    }
+    if (order == MPIX_ORDER_TREE && (n & (n - 1))) {
+        MPIR_Err_set_detail("MPIX_ORDER_TREE needs a power-of-two operand count");
+        return err_return(fc, MPI_ERR_ARG);
+    }
+    for (j = 0; j < n; j++) {
+        mpi_errno = validate(inbufs[j], outbuf, j == 0 ? 0 : count, datatype, op);
+        if (mpi_errno != MPI_SUCCESS)
+            return err_return(fc, mpi_errno);
+    }
+    if (count <= 0)
+        return MPI_SUCCESS;
+    if (HANDLE_GET_KIND(op) != HANDLE_KIND_BUILTIN) {
+        MPIR_Err_set_detail("user MPI_Op functions run on the host; use MPI_Reduce_local");
+        return err_return(fc, MPI_ERR_OP);
+    }
+    opidx = op & 0xf;
+    elem = MPIR_Op_resolve_elem(opidx, datatype);
+    if (!elem) {
+        MPIR_Err_set_detail("MPI_Op operation not defined for this datatype");
+        return err_return(fc, MPI_ERR_OP);
+    }
+    rc = MPIR_Hip_combine(inbufs, n, outbuf, (uint64_t) count, opidx, elem,
+                          order == MPIX_ORDER_TREE ? MPIR_HIP_ORDER_TREE : MPIR_HIP_ORDER_CHAIN,
+                          hip_stream, hip_stream == NULL);
+    if (rc == MPIR_HIP_EBUFFER) {
+        MPIR_Err_set_detail("%s needs device-resident buffers on one device", fc);
+        return err_return(fc, MPI_ERR_BUFFER);
+    }
+    if (rc != MPIR_HIP_OK) {
+        MPIR_Op_report_hip_error(fc, rc);
+        return err_return(fc, *MPIR_Op_errno_ptr());
+    }
+    return MPI_SUCCESS;
+}
+
 /* ---- MPI_Op_create / MPI_Op_free / MPI_Op_commutative ------------------ */
 int PMPI_Op_create(MPI_User_function * user_fn, int commute, MPI_Op * op)
 {

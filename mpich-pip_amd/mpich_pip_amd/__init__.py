@@ -107,6 +107,7 @@ EXPORTED_SYMBOLS = [
     "MPI_Op_commutative", "PMPI_Op_commutative", "MPIR_Op_is_commutative",
     "MPI_Error_class", "MPI_Error_string",
     "MPIX_Reduce_local_stream", "MPIX_Reduce_local_set_errhandler", "MPIX_Reduce_local_get_errhandler",
+    "MPIX_Reduce_local_multi", "MPIR_Hip_combine",
     # the HIP shim (include/mpir_hip_reduce.h)
     "MPIR_Hip_reduce", "MPIR_Hip_elem_size", "MPIR_Hip_has_kernel", "MPIR_Hip_is_device_ptr",
     "MPIR_Hip_memcpy", "MPIR_Hip_error_string", "MPIR_Hip_device_count",
@@ -135,6 +136,8 @@ def load(path: str | None = None) -> ctypes.CDLL:
         f.restype = i32
     lib.MPIX_Reduce_local_stream.argtypes = [vp, vp, i32, i32, i32, vp]
     lib.MPIX_Reduce_local_stream.restype = i32
+    lib.MPIX_Reduce_local_multi.argtypes = [ctypes.POINTER(vp), i32, vp, i32, i32, i32, i32, vp]
+    lib.MPIX_Reduce_local_multi.restype = i32
     lib.MPIX_Reduce_local_set_errhandler.argtypes = [i32]
     lib.MPIX_Reduce_local_set_errhandler.restype = i32
     lib.MPI_Op_create.argtypes = [MPI_User_function, i32, ctypes.POINTER(i32)]
@@ -175,6 +178,18 @@ def error_string(code: int) -> str:
 def reduce_local(inbuf: int, inoutbuf: int, count: int, datatype: int, op: int) -> int:
     """MPI_Reduce_local on raw addresses (device or host)."""
     return load().MPI_Reduce_local(ctypes.c_void_p(inbuf), ctypes.c_void_p(inoutbuf), count, datatype, op)
+
+
+MPIX_ORDER_TREE = 0
+MPIX_ORDER_CHAIN = 1
+
+
+def reduce_local_multi(inbufs, outbuf: int, count: int, datatype: int, op: int, order: int,
+                       stream: int = 0) -> int:
+    """MPIX_Reduce_local_multi: outbuf = tree/chain fold of device buffers (addresses)."""
+    arr = (ctypes.c_void_p * len(inbufs))(*inbufs)
+    return load().MPIX_Reduce_local_multi(arr, len(inbufs), ctypes.c_void_p(outbuf), count, datatype, op, order,
+                                          ctypes.c_void_p(stream or None))
 
 
 def reduce_local_stream(inbuf: int, inoutbuf: int, count: int, datatype: int, op: int, stream: int = 0) -> int:

@@ -1,0 +1,127 @@
+"""Fused schedule combines (MPIX_Reduce_local_multi) vs the reference schedules, on one GPU.
+
+The reference's Allreduce on one node (allreduce_intra_smp.c -> MPIR_Reduce via
+reduce_intra_reduce_scatter_gather.c) and its Reduce_scatter_block
+(reduce_scatter_block_intra_pairwise.c) call MPIR_Reduce_local log2(p) resp.
+p-1 times per element.  The MI355X design gathers every rank's copy of a block
+in HBM (all-to-all) and folds them in ONE pass with the schedule's exact
+association and operand order.  Here p ranks' buffers live on one GPU; the
+expected bytes come from oracle/schedules.py, which runs the reference
+schedules step by step through the C oracle.  Bit-exact (complex NaN payloads
+excepted, see test_parity_gpu.same).
+"""
+import numpy as np
+import pytest
+
+import _types as T
+from test_parity_gpu import same
+
+pytestmark = pytest.mark.gpu
+
+
+def _pof2(p):
+    q = 1
+    while q * 2 <= p:
+        q *= 2
+    return q
+
+
+def _cnts_disps(count, pof2):
+    cnts = [count // pof2 + (1 if i < count % pof2 else 0) for i in range(pof2)]
+    disps = [sum(cnts[:i]) for i in range(pof2)]
+    return cnts, disps
+
+
+def _bitrev(n, bits):
+    return int(format(n, f"0{bits}b")[::-1], 2) if bits else 0
+
+
+def fused_allreduce(mpi, torch, xs_dev, count, esz, dt, op):
+    """The MI355X reference-order Allreduce on p virtual ranks (one GPU):
+    pre-fold (p not a power of two), then per block b the owner newrank
+    k = bitrev(b) folds y_j = x_{k ^ j}[b] with MPIX_ORDER_TREE."""
+    p = len(xs_dev)
+    pof2 = _pof2(p)
+    rem = p - pof2
+    leaves = []
+    for r in range(p):                     # reduce_intra_reduce_scatter_gather.c:138-170
+        if r < 2 * rem:
+            if r % 2 == 0:
+                acc = xs_dev[r].clone()
+                torch.cuda.synchronize()
+                assert mpi.reduce_local(xs_dev[r + 1].data_ptr(), acc.data_ptr(), count, dt, op) == 0
+                leaves.append(acc)
+        else:
+            leaves.append(xs_dev[r])
+    assert len(leaves) == pof2
+    cnts, disps = _cnts_disps(count, pof2)
+    out = torch.empty(count * esz, dtype=torch.uint8, device="cuda")
+    bits = pof2.bit_length() - 1
+    for b in range(pof2):
+        k = _bitrev(b, bits)
+        ys = [leaves[k ^ j].data_ptr() + disps[b] * esz for j in range(pof2)]
+        rc = mpi.reduce_local_multi(ys, out.data_ptr() + disps[b] * esz, cnts[b], dt, op, mpi.MPIX_ORDER_TREE)
+        assert rc == 0, mpi.error_string(rc)
+    torch.cuda.synchronize()
+    return out.cpu().numpy()
+
+
+CASES = [("MPI_FLOAT", "MPI_SUM"), ("MPI_DOUBLE", "MPI_SUM"), ("MPIX_C_FLOAT16", "MPI_SUM"),
+         ("MPI_INT", "MPI_SUM"), ("MPI_INT64_T", "MPI_PROD"), ("MPI_FLOAT", "MPI_MAX"),
+         ("MPI_DOUBLE", "MPI_MIN"), ("MPI_C_FLOAT_COMPLEX", "MPI_SUM"), ("MPI_FLOAT", "MPI_PROD"),
+         ("MPI_UNSIGNED_CHAR", "MPI_BXOR"), ("MPI_INT", "MPI_LAND")]
+
+
+@pytest.mark.parametrize("t,op", CASES, ids=[f"{t}-{o}" for t, o in CASES])
+@pytest.mark.parametrize("p", [2, 3, 4, 6, 8])
+def test_fused_allreduce_matches_reference_schedule(mpi, orc, cuda, t, op, p):
+    from oracle import schedules as S
+    torch = cuda
+    esz = T.elem_size(t)
+    for count, seed in ((1003, p), ((1 << 18) + 5, 7 * p)):
+        rng = np.random.default_rng(seed)
+        xs = [T.to_bytes(T.gen(t, count, rng, op)) for _ in range(p)]
+        want = S.allreduce_smp(xs, count, esz, mpi.DATATYPES[t], mpi.OPS[op])
+        xs_dev = [torch.from_numpy(x.copy()).cuda() for x in xs]
+        got = fused_allreduce(mpi, torch, xs_dev, count, esz, mpi.DATATYPES[t], mpi.OPS[op])
+        assert same(got, want, t), f"p={p} count={count}: {np.count_nonzero(got != want)} bytes differ"
+
+
+@pytest.mark.parametrize("t,op", [("MPIX_C_FLOAT16", "MPI_SUM"), ("MPI_FLOAT", "MPI_SUM"), ("MPI_INT", "MPI_SUM"),
+                                  ("MPI_DOUBLE", "MPI_MAX"), ("MPI_UNSIGNED", "MPI_BOR")])
+@pytest.mark.parametrize("p", [2, 3, 5, 8, 11])
+def test_fused_reduce_scatter_block_matches_pairwise(mpi, orc, cuda, t, op, p):
+    """Config 5's schedule: rank r's block = ((x_r + x_{r-1}) + x_{r-2}) + ... (fp16: per-step rounding)."""
+    from oracle import schedules as S
+    torch = cuda
+    esz = T.elem_size(t)
+    recvcount = 4099
+    rng = np.random.default_rng(p)
+    xs = [T.to_bytes(T.gen(t, recvcount * p, rng, op)) for _ in range(p)]
+    want = S.reduce_scatter_block_pairwise(xs, recvcount, esz, mpi.DATATYPES[t], mpi.OPS[op])
+    xs_dev = [torch.from_numpy(x.copy()).cuda() for x in xs]
+    nb = recvcount * esz
+    for r in range(p):
+        out = torch.empty(nb, dtype=torch.uint8, device="cuda")
+        ys = [xs_dev[(r - i) % p].data_ptr() + r * nb for i in range(p)]
+        rc = mpi.reduce_local_multi(ys, out.data_ptr(), recvcount, mpi.DATATYPES[t], mpi.OPS[op],
+                                    mpi.MPIX_ORDER_CHAIN)
+        assert rc == 0, mpi.error_string(rc)
+        got = out.cpu().numpy()
+        assert same(got, want[r], t), f"rank {r}"
+
+
+def test_multi_validation(mpi, cuda):
+    torch = cuda
+    a = torch.zeros(64, device="cuda")
+    b = torch.zeros(64, device="cuda")
+    ptrs = [a.data_ptr(), b.data_ptr(), a.data_ptr()]
+    # tree needs a power of two
+    assert mpi.reduce_local_multi(ptrs, b.data_ptr(), 64, mpi.MPI_FLOAT, mpi.MPI_SUM,
+                                  mpi.MPIX_ORDER_TREE) == mpi.MPI_ERR_ARG
+    # op/type check like MPI_Reduce_local
+    assert mpi.reduce_local_multi(ptrs[:2], b.data_ptr(), 64, mpi.MPI_FLOAT, mpi.MPI_BAND,
+                                  mpi.MPIX_ORDER_CHAIN) == mpi.MPI_ERR_OP
+    h = np.zeros(64, np.float32)
+    assert mpi.reduce_local_multi([h.ctypes.data, a.data_ptr()], b.data_ptr(), 64, mpi.MPI_FLOAT, mpi.MPI_SUM,
+                                  mpi.MPIX_ORDER_CHAIN) == mpi.MPI_ERR_BUFFER
