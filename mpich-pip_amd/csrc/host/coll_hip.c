@@ -1,0 +1,663 @@
+/*
+ * coll_hip.c -- device reduction collectives over RCCL / an in-process
+ * loopback, built on the gfx950 MPIR_Reduce_local kernels.  See
+ * include/mpix_hip_coll.h for the contract.
+ *
+ * Reference schedules reproduced (bit-identical results):
+ *   Allreduce, one node: allreduce_intra_smp.c (MPIR_Reduce to node root via
+ *     reduce_intra_reduce_scatter_gather.c:130-250, then MPIR_Bcast).
+ *     Non-power-of-two pre-fold :138-170 (odd rank r < 2*rem sends to r-1,
+ *     even computes x_r (+) x_{r+1}); recursive halving :186-249 leaves newrank
+ *     n owning block bitrev(n), reduced as ((y0+y1)+(y2+y3))+... with
+ *     y_j = contribution of newrank n ^ j (tests/test_schedule_fused_gpu.py).
+ *   Reduce_scatter_block: reduce_scatter_block_intra_pairwise.c:75-134:
+ *     block r = ((x_r + x_{r-1}) + x_{r-2}) + ... .
+ * MI355X form: the log2(p) Sendrecv+Reduce_local rounds become one all-to-all
+ * (every xGMI link busy at once) + one fused combine pass + one allgather.
+ */
+#include <dlfcn.h>
+#include <pthread.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <hip/hip_runtime_api.h>
+#include <rccl/rccl.h>
+
+#include "mpix_hip_coll.h"
+#include "mpir_op_types.h"
+
+#define COMM_RCCL 1
+#define COMM_LOOPBACK 2
+#define MAX_XFER 256
+
+typedef struct {
+    void *buf;
+    size_t bytes;
+    int peer;
+} xfer_t;
+
+/* ------------------------------------------------------------ RCCL (dlopen) */
+static struct {
+    int loaded;
+    void *so;
+    ncclResult_t (*GetUniqueId)(ncclUniqueId *);
+    ncclResult_t (*CommInitRank)(ncclComm_t *, int, ncclUniqueId, int);
+    ncclResult_t (*CommDestroy)(ncclComm_t);
+    ncclResult_t (*AllReduce)(const void *, void *, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t, hipStream_t);
+    ncclResult_t (*ReduceScatter)(const void *, void *, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t,
+                                  hipStream_t);
+    ncclResult_t (*Send)(const void *, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t);
+    ncclResult_t (*Recv)(void *, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t);
+    ncclResult_t (*GroupStart)(void);
+    ncclResult_t (*GroupEnd)(void);
+    const char *(*GetErrorString)(ncclResult_t);
+} rccl;
+static pthread_mutex_t rccl_lock = PTHREAD_MUTEX_INITIALIZER;
+
+static int rccl_load(void)
+{
+    static const char *names[] = { "librccl.so.1", "/opt/rocm/lib/librccl.so.1", "librccl.so" };
+    size_t i;
+    pthread_mutex_lock(&rccl_lock);
+    if (rccl.loaded) {
+        pthread_mutex_unlock(&rccl_lock);
+        return rccl.loaded > 0;
+    }
+    for (i = 0; i < sizeof(names) / sizeof(names[0]) && !rccl.so; i++)
+        rccl.so = dlopen(names[i], RTLD_NOW | RTLD_GLOBAL);
+    if (rccl.so) {
+#define SYM(f, n) *(void **) (&rccl.f) = dlsym(rccl.so, n)
+        SYM(GetUniqueId, "ncclGetUniqueId");
+        SYM(CommInitRank, "ncclCommInitRank");
+        SYM(CommDestroy, "ncclCommDestroy");
+        SYM(AllReduce, "ncclAllReduce");
+        SYM(ReduceScatter, "ncclReduceScatter");
+        SYM(Send, "ncclSend");
+        SYM(Recv, "ncclRecv");
+        SYM(GroupStart, "ncclGroupStart");
+        SYM(GroupEnd, "ncclGroupEnd");
+        SYM(GetErrorString, "ncclGetErrorString");
+#undef SYM
+    }
+    rccl.loaded = (rccl.so && rccl.GetUniqueId && rccl.CommInitRank && rccl.Send && rccl.Recv &&
+                   rccl.GroupStart && rccl.GroupEnd && rccl.AllReduce && rccl.ReduceScatter) ? 1 : -1;
+    pthread_mutex_unlock(&rccl_lock);
+    return rccl.loaded > 0;
+}
+
+/* ------------------------------------------------------------ communicators */
+typedef struct loop_hub {
+    int size;
+    int refs;
+    pthread_barrier_t bar;
+    pthread_mutex_t lock;
+    struct {
+        int nsend;
+        xfer_t sends[MAX_XFER];
+        hipEvent_t ready;
+    } slot[64];
+} loop_hub_t;
+
+struct MPIX_Hip_comm_s {
+    int kind, rank, size, device;
+    hipStream_t stream;
+    void *scratch;
+    size_t scratch_bytes;
+    ncclComm_t nccl;
+    loop_hub_t *hub;
+};
+
+static int hip_fail(const char *fc, hipError_t e)
+{
+    MPIR_Err_set_detail("%s: HIP error %s", fc, hipGetErrorString(e));
+    return MPIR_Err_return(fc, MPI_ERR_OTHER);
+}
+
+static int comm_init_common(struct MPIX_Hip_comm_s *c)
+{
+    hipError_t e = hipGetDevice(&c->device);
+    if (e == hipSuccess)
+        e = hipStreamCreate(&c->stream);
+    return e == hipSuccess ? 0 : (int) e;
+}
+
+int MPIX_Hip_comm_get_unique_id(void *id)
+{
+    ncclUniqueId u;
+    ncclResult_t r;
+    if (!rccl_load()) {
+        MPIR_Err_set_detail("RCCL (librccl.so.1) could not be loaded");
+        return MPIR_Err_return("MPIX_Hip_comm_get_unique_id", MPI_ERR_OTHER);
+    }
+    r = rccl.GetUniqueId(&u);
+    if (r != ncclSuccess) {
+        MPIR_Err_set_detail("ncclGetUniqueId: %s", rccl.GetErrorString ? rccl.GetErrorString(r) : "?");
+        return MPIR_Err_return("MPIX_Hip_comm_get_unique_id", MPI_ERR_OTHER);
+    }
+    memcpy(id, &u, sizeof(u));
+    return MPI_SUCCESS;
+}
+
+int MPIX_Hip_comm_create(const void *id, int size, int rank, MPIX_Hip_comm * comm)
+{
+    static const char *fc = "MPIX_Hip_comm_create";
+    struct MPIX_Hip_comm_s *c;
+    ncclUniqueId u;
+    ncclResult_t r;
+    int e;
+    if (size < 1 || rank < 0 || rank >= size || size > 64) {
+        MPIR_Err_set_detail("%s: invalid size/rank", fc);
+        return MPIR_Err_return(fc, MPI_ERR_ARG);
+    }
+    if (!rccl_load()) {
+        MPIR_Err_set_detail("RCCL (librccl.so.1) could not be loaded");
+        return MPIR_Err_return(fc, MPI_ERR_OTHER);
+    }
+    c = calloc(1, sizeof(*c));
+    c->kind = COMM_RCCL;
+    c->rank = rank;
+    c->size = size;
+    if ((e = comm_init_common(c)) != 0) {
+        free(c);
+        return hip_fail(fc, (hipError_t) e);
+    }
+    memcpy(&u, id, sizeof(u));
+    r = rccl.CommInitRank(&c->nccl, size, u, rank);
+    if (r != ncclSuccess) {
+        MPIR_Err_set_detail("ncclCommInitRank: %s", rccl.GetErrorString ? rccl.GetErrorString(r) : "?");
+        (void) hipStreamDestroy(c->stream);
+        free(c);
+        return MPIR_Err_return(fc, MPI_ERR_OTHER);
+    }
+    *comm = c;
+    return MPI_SUCCESS;
+}
+
+int MPIX_Hip_comm_create_loopback(int size, MPIX_Hip_comm * comms)
+{
+    static const char *fc = "MPIX_Hip_comm_create_loopback";
+    loop_hub_t *hub;
+    int r, e;
+    if (size < 1 || size > 64) {
+        MPIR_Err_set_detail("%s: size must be 1..64", fc);
+        return MPIR_Err_return(fc, MPI_ERR_ARG);
+    }
+    hub = calloc(1, sizeof(*hub));
+    hub->size = size;
+    hub->refs = size;
+    pthread_barrier_init(&hub->bar, NULL, (unsigned) size);
+    pthread_mutex_init(&hub->lock, NULL);
+    for (r = 0; r < size; r++) {
+        struct MPIX_Hip_comm_s *c = calloc(1, sizeof(*c));
+        c->kind = COMM_LOOPBACK;
+        c->rank = r;
+        c->size = size;
+        c->hub = hub;
+        if ((e = comm_init_common(c)) != 0)
+            return hip_fail(fc, (hipError_t) e);
+        if ((e = hipEventCreateWithFlags(&hub->slot[r].ready, hipEventDisableTiming)) != hipSuccess)
+            return hip_fail(fc, (hipError_t) e);
+        comms[r] = c;
+    }
+    return MPI_SUCCESS;
+}
+
+int MPIX_Hip_comm_free(MPIX_Hip_comm * comm)
+{
+    struct MPIX_Hip_comm_s *c = *comm;
+    if (!c)
+        return MPI_SUCCESS;
+    (void) hipStreamSynchronize(c->stream);
+    if (c->kind == COMM_RCCL && c->nccl && rccl.CommDestroy)
+        rccl.CommDestroy(c->nccl);
+    if (c->kind == COMM_LOOPBACK) {
+        loop_hub_t *hub = c->hub;
+        int last;
+        pthread_mutex_lock(&hub->lock);
+        last = --hub->refs == 0;
+        pthread_mutex_unlock(&hub->lock);
+        if (last) {
+            int r;
+            for (r = 0; r < hub->size; r++)
+                (void) hipEventDestroy(hub->slot[r].ready);
+            pthread_barrier_destroy(&hub->bar);
+            pthread_mutex_destroy(&hub->lock);
+            free(hub);
+        }
+    }
+    if (c->scratch)
+        (void) hipFree(c->scratch);
+    (void) hipStreamDestroy(c->stream);
+    free(c);
+    *comm = NULL;
+    return MPI_SUCCESS;
+}
+
+int MPIX_Hip_comm_rank(MPIX_Hip_comm comm, int *rank)
+{
+    *rank = comm->rank;
+    return MPI_SUCCESS;
+}
+
+int MPIX_Hip_comm_size(MPIX_Hip_comm comm, int *size)
+{
+    *size = comm->size;
+    return MPI_SUCCESS;
+}
+
+static int comm_scratch(struct MPIX_Hip_comm_s *c, size_t bytes, char **out)
+{
+    if (c->scratch_bytes < bytes) {
+        hipError_t e;
+        if (c->scratch) {
+            (void) hipStreamSynchronize(c->stream);
+            (void) hipDeviceSynchronize();
+            (void) hipFree(c->scratch);
+        }
+        c->scratch = NULL;
+        c->scratch_bytes = 0;
+        e = hipMalloc(&c->scratch, bytes);
+        if (e != hipSuccess)
+            return (int) e;
+        c->scratch_bytes = bytes;
+    }
+    *out = c->scratch;
+    return 0;
+}
+
+/* ------------------------------------------------------------ transport:
+ * one group of point-to-point transfers that progress together (all xGMI
+ * links at once); completes in stream order. */
+static int group_exchange(struct MPIX_Hip_comm_s *c, const xfer_t *sends, int nsend, const xfer_t *recvs,
+                          int nrecv, hipStream_t s)
+{
+    int i, j;
+    if (c->kind == COMM_RCCL) {
+        ncclResult_t r = rccl.GroupStart();
+        for (i = 0; i < nsend && r == ncclSuccess; i++)
+            if (sends[i].bytes)
+                r = rccl.Send(sends[i].buf, sends[i].bytes, ncclUint8, sends[i].peer, c->nccl, s);
+        for (i = 0; i < nrecv && r == ncclSuccess; i++)
+            if (recvs[i].bytes)
+                r = rccl.Recv(recvs[i].buf, recvs[i].bytes, ncclUint8, recvs[i].peer, c->nccl, s);
+        {
+            ncclResult_t r2 = rccl.GroupEnd();
+            if (r == ncclSuccess)
+                r = r2;
+        }
+        if (r != ncclSuccess) {
+            MPIR_Err_set_detail("RCCL grouped send/recv: %s", rccl.GetErrorString ? rccl.GetErrorString(r) : "?");
+            return MPI_ERR_OTHER;
+        }
+        return MPI_SUCCESS;
+    } else {
+        /* loopback: post sends + a ready event; every receiver copies from the
+         * matching sender once that event has fired; barrier both sides so no
+         * sender reuses a buffer before its readers are done */
+        loop_hub_t *hub = c->hub;
+        hipError_t e;
+        if (nsend > MAX_XFER)
+            return MPI_ERR_INTERN;
+        hub->slot[c->rank].nsend = nsend;
+        memcpy(hub->slot[c->rank].sends, sends, sizeof(xfer_t) * (size_t) nsend);
+        e = hipEventRecord(hub->slot[c->rank].ready, s);
+        pthread_barrier_wait(&hub->bar);
+        for (i = 0; i < nrecv && e == hipSuccess; i++) {
+            int peer = recvs[i].peer, found = 0;
+            for (j = 0; j < hub->slot[peer].nsend; j++) {
+                const xfer_t *x = &hub->slot[peer].sends[j];
+                if (x->peer == c->rank) {
+                    if (x->bytes != recvs[i].bytes) {
+                        MPIR_Err_set_detail("loopback: size mismatch %zu vs %zu", x->bytes, recvs[i].bytes);
+                        pthread_barrier_wait(&hub->bar);
+                        return MPI_ERR_INTERN;
+                    }
+                    e = hipStreamWaitEvent(s, hub->slot[peer].ready, 0);
+                    if (e == hipSuccess && x->bytes)
+                        e = hipMemcpyAsync(recvs[i].buf, x->buf, x->bytes, hipMemcpyDeviceToDevice, s);
+                    found = 1;
+                    break;
+                }
+            }
+            if (!found && recvs[i].bytes) {
+                MPIR_Err_set_detail("loopback: no matching send from %d", peer);
+                pthread_barrier_wait(&hub->bar);
+                return MPI_ERR_INTERN;
+            }
+        }
+        if (e == hipSuccess)
+            e = hipStreamSynchronize(s);
+        pthread_barrier_wait(&hub->bar);
+        if (e != hipSuccess) {
+            MPIR_Err_set_detail("loopback transfer: %s", hipGetErrorString(e));
+            return MPI_ERR_OTHER;
+        }
+        return MPI_SUCCESS;
+    }
+}
+
+/* ------------------------------------------------------------ helpers */
+static int pof2_of(int p)
+{
+    int q = 1;
+    while (q * 2 <= p)
+        q *= 2;
+    return q;
+}
+
+static int bitrev(int n, int bits)
+{
+    int r = 0, i;
+    for (i = 0; i < bits; i++)
+        if (n & (1 << i))
+            r |= 1 << (bits - 1 - i);
+    return r;
+}
+
+static void cnts_disps(long count, int pof2, long *cnts, long *disps)
+{
+    int i;
+    for (i = 0; i < pof2; i++)
+        cnts[i] = count / pof2 + (i < count % pof2 ? 1 : 0);
+    disps[0] = 0;
+    for (i = 1; i < pof2; i++)
+        disps[i] = disps[i - 1] + cnts[i - 1];
+}
+
+/* validation shared by both collectives (MPIR_ERRTEST_OP + check_dtype) */
+static int coll_check(const char *fc, const void *sendbuf, void *recvbuf, int count, MPI_Datatype dt, MPI_Op op,
+                      MPIX_Hip_comm comm, int *elem)
+{
+    unsigned kind = ((unsigned) op & 0xc0000000u) >> 30, mpikind = ((unsigned) op & 0x3c000000u) >> 26;
+    int opidx = op & 0xf, rc;
+    if (!comm) {
+        MPIR_Err_set_detail("%s: null communicator", fc);
+        return MPI_ERR_ARG;
+    }
+    if (count < 0) {
+        MPIR_Err_set_detail("%s: negative count", fc);
+        return MPI_ERR_COUNT;
+    }
+    if (op == MPI_OP_NULL || op == MPI_NO_OP || op == MPI_REPLACE || kind != 1 || mpikind != 6 ||
+        opidx < 1 || opidx > 12) {
+        MPIR_Err_set_detail("%s: builtin reduction MPI_Op required", fc);
+        return MPI_ERR_OP;
+    }
+    if ((rc = MPIR_Op_check_dtype_table[opidx] (dt)) != MPI_SUCCESS)
+        return rc;
+    *elem = MPIR_Op_resolve_elem(opidx, dt);
+    if (!*elem) {
+        MPIR_Err_set_detail("MPI_Op operation not defined for this datatype");
+        return MPI_ERR_OP;
+    }
+    if (count > 0 && sendbuf == recvbuf) {
+        MPIR_Err_set_detail("%s: Buffers must not be aliased", fc);
+        return MPI_ERR_BUFFER;
+    }
+    return MPI_SUCCESS;
+}
+
+static int want_rccl(struct MPIX_Hip_comm_s *c, int algorithm, int elem, int opidx, ncclDataType_t * t,
+                     ncclRedOp_t * o)
+{
+    const char *v;
+    if (c->kind != COMM_RCCL || algorithm == MPIX_HIP_ALG_REFERENCE_ORDER)
+        return 0;
+    if (algorithm == MPIX_HIP_ALG_AUTO && (v = getenv("MPIR_CVAR_DEVICE_COLL_ALGORITHM")) &&
+        !strcmp(v, "reference"))
+        return 0;
+    switch (elem) {
+    case MPIR_HIP_I8: *t = ncclInt8; break;
+    case MPIR_HIP_U8: *t = ncclUint8; break;
+    case MPIR_HIP_I32: *t = ncclInt32; break;
+    case MPIR_HIP_U32: *t = ncclUint32; break;
+    case MPIR_HIP_I64: *t = ncclInt64; break;
+    case MPIR_HIP_U64: *t = ncclUint64; break;
+    case MPIR_HIP_F16: *t = ncclFloat16; break;
+    case MPIR_HIP_F32: *t = ncclFloat32; break;
+    case MPIR_HIP_F64: *t = ncclFloat64; break;
+    default: return 0;
+    }
+    switch (opidx) {
+    case MPIR_HIP_OP_SUM: *o = ncclSum; break;
+    case MPIR_HIP_OP_PROD: *o = ncclProd; break;
+    case MPIR_HIP_OP_MAX: *o = ncclMax; break;
+    case MPIR_HIP_OP_MIN: *o = ncclMin; break;
+    default: return 0;
+    }
+    return 1;
+}
+
+#define HIPTRY(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { \
+        MPIR_Err_set_detail("%s: %s", #x, hipGetErrorString(e_)); rc = MPI_ERR_OTHER; goto done; } } while (0)
+#define TRY(x) do { if ((rc = (x)) != MPI_SUCCESS) goto done; } while (0)
+
+/* ------------------------------------------------------------ Allreduce */
+int MPIX_Allreduce_hip(const void *sendbuf, void *recvbuf, int count, MPI_Datatype datatype, MPI_Op op,
+                       MPIX_Hip_comm comm, int algorithm, void *hip_stream)
+{
+    static const char *fc = "MPIX_Allreduce_hip";
+    struct MPIX_Hip_comm_s *c = comm;
+    int elem = 0, opidx = op & 0xf, rc, p, pof2, rem, newrank, bits, i;
+    size_t esz, bytes;
+    hipStream_t s;
+    ncclDataType_t nt;
+    ncclRedOp_t no;
+    long cnts[64] = {0}, disps[64] = {0}, maxblk;
+    xfer_t sends[MAX_XFER], recvs[MAX_XFER];
+    int nsend = 0, nrecv = 0, cur = 0;
+    char *scr = NULL;
+
+    rc = coll_check(fc, sendbuf, recvbuf, count, datatype, op, comm, &elem);
+    if (rc)
+        return MPIR_Err_return(fc, rc);
+    if (count == 0)
+        return MPI_SUCCESS;
+    if (hipGetDevice(&cur) == hipSuccess && cur != c->device)
+        (void) hipSetDevice(c->device);
+    s = hip_stream ? (hipStream_t) hip_stream : c->stream;
+    esz = MPIR_Hip_elem_size(elem);
+    bytes = (size_t) count * esz;
+    p = c->size;
+
+    if (want_rccl(c, algorithm, elem, opidx, &nt, &no)) {
+        ncclResult_t r = rccl.AllReduce(sendbuf == MPI_IN_PLACE ? recvbuf : sendbuf, recvbuf, (size_t) count,
+                                        nt, no, c->nccl, s);
+        if (r != ncclSuccess) {
+            MPIR_Err_set_detail("ncclAllReduce: %s", rccl.GetErrorString ? rccl.GetErrorString(r) : "?");
+            rc = MPI_ERR_OTHER;
+        }
+        goto done_sync;
+    }
+
+    /* ---- reference order (allreduce_intra_smp.c + reduce_intra_reduce_scatter_gather.c) */
+    if (sendbuf != MPI_IN_PLACE)
+        HIPTRY(hipMemcpyAsync(recvbuf, sendbuf, bytes, hipMemcpyDeviceToDevice, s));
+    pof2 = pof2_of(p);
+    rem = p - pof2;
+    bits = 0;
+    while ((1 << bits) < pof2)
+        bits++;
+    cnts_disps(count, pof2, cnts, disps);
+    maxblk = cnts[0];
+    if (comm_scratch(c, (size_t) (pof2 > 1 ? pof2 - 1 : 1) * (size_t) maxblk * esz + bytes + 256, &scr)) {
+        MPIR_Err_set_detail("%s: scratch allocation failed", fc);
+        rc = MPI_ERR_NO_MEM;
+        goto done;
+    }
+    /* pre-fold (reduce_intra_reduce_scatter_gather.c:138-170); every rank takes
+     * part in the transfer group (empty for ranks >= 2*rem) */
+    if (rem > 0 && c->rank >= 2 * rem)
+        TRY(group_exchange(c, NULL, 0, NULL, 0, s));
+    if (c->rank < 2 * rem) {
+        if (c->rank % 2) {
+            xfer_t x = { recvbuf, bytes, c->rank - 1 };
+            TRY(group_exchange(c, &x, 1, NULL, 0, s));
+            newrank = -1;
+        } else {
+            char *tmp = scr + (size_t) (pof2 > 1 ? pof2 - 1 : 1) * (size_t) maxblk * esz;
+            xfer_t x = { tmp, bytes, c->rank + 1 };
+            TRY(group_exchange(c, NULL, 0, &x, 1, s));
+            rc = MPIR_Hip_reduce(tmp, recvbuf, (uint64_t) count, opidx, elem, s, 0);
+            if (rc) {
+                MPIR_Op_report_hip_error(fc, rc);
+                rc = MPI_ERR_OTHER;
+                goto done;
+            }
+            newrank = c->rank / 2;
+        }
+    } else
+        newrank = c->rank - rem;
+
+    /* all-to-all of blocks: newrank n owns block bitrev(n) (recursive halving,
+     * :186-249); the owner receives y_j = block from newrank n ^ j into slot j-1 */
+    if (newrank >= 0 && pof2 > 1) {
+        int mb = bitrev(newrank, bits), m;
+        const void *ys[64];
+        nsend = nrecv = 0;
+        for (m = 0; m < pof2; m++) {
+            int real, b;
+            if (m == newrank)
+                continue;
+            real = m < rem ? 2 * m : m + rem;
+            b = bitrev(m, bits);
+            sends[nsend].buf = (char *) recvbuf + disps[b] * esz;
+            sends[nsend].bytes = (size_t) cnts[b] * esz;
+            sends[nsend++].peer = real;
+            recvs[nrecv].buf = scr + (size_t) ((newrank ^ m) - 1) * (size_t) maxblk * esz;
+            recvs[nrecv].bytes = (size_t) cnts[mb] * esz;
+            recvs[nrecv++].peer = real;
+        }
+        TRY(group_exchange(c, sends, nsend, recvs, nrecv, s));
+        ys[0] = (char *) recvbuf + disps[mb] * esz;
+        for (i = 1; i < pof2; i++)
+            ys[i] = scr + (size_t) (i - 1) * (size_t) maxblk * esz;
+        if (cnts[mb]) {
+            rc = MPIR_Hip_combine(ys, pof2, (char *) recvbuf + disps[mb] * esz, (uint64_t) cnts[mb], opidx, elem,
+                                  MPIR_HIP_ORDER_TREE, s, 0);
+            if (rc) {
+                MPIR_Op_report_hip_error(fc, rc);
+                rc = MPI_ERR_OTHER;
+                goto done;
+            }
+        }
+    } else if (newrank < 0 && pof2 > 1) {
+        /* excluded rank: matches the group call of the participants (no transfers) */
+        TRY(group_exchange(c, NULL, 0, NULL, 0, s));
+    }
+
+    /* allgather of the reduced blocks to every rank (the gather + MPIR_Bcast of
+     * allreduce_intra_smp.c move data only) */
+    nsend = nrecv = 0;
+    if (newrank >= 0) {
+        int mb = bitrev(newrank, bits), q;
+        for (q = 0; q < p; q++) {
+            if (q == c->rank)
+                continue;
+            sends[nsend].buf = (char *) recvbuf + disps[mb] * esz;
+            sends[nsend].bytes = (size_t) cnts[mb] * esz;
+            sends[nsend++].peer = q;
+        }
+    }
+    for (i = 0; i < pof2; i++) {
+        int real = i < rem ? 2 * i : i + rem, b = bitrev(i, bits);
+        if (real == c->rank)
+            continue;
+        recvs[nrecv].buf = (char *) recvbuf + disps[b] * esz;
+        recvs[nrecv].bytes = (size_t) cnts[b] * esz;
+        recvs[nrecv++].peer = real;
+    }
+    if (p > 1)
+        TRY(group_exchange(c, sends, nsend, recvs, nrecv, s));
+
+  done_sync:
+    if (rc == MPI_SUCCESS && !hip_stream)
+        HIPTRY(hipStreamSynchronize(s));
+  done:
+    if (cur != c->device)
+        (void) hipSetDevice(cur);
+    return rc ? MPIR_Err_return(fc, rc) : MPI_SUCCESS;
+}
+
+/* ------------------------------------------------------------ Reduce_scatter_block */
+int MPIX_Reduce_scatter_block_hip(const void *sendbuf, void *recvbuf, int recvcount, MPI_Datatype datatype,
+                                  MPI_Op op, MPIX_Hip_comm comm, int algorithm, void *hip_stream)
+{
+    static const char *fc = "MPIX_Reduce_scatter_block_hip";
+    struct MPIX_Hip_comm_s *c = comm;
+    int elem = 0, opidx = op & 0xf, rc, p, i, cur = 0;
+    size_t esz, nb;
+    hipStream_t s;
+    ncclDataType_t nt;
+    ncclRedOp_t no;
+    xfer_t sends[MAX_XFER], recvs[MAX_XFER];
+    const void *ys[64];
+    const char *src;
+    char *scr = NULL;
+
+    rc = coll_check(fc, sendbuf, recvbuf, recvcount, datatype, op, comm, &elem);
+    if (rc)
+        return MPIR_Err_return(fc, rc);
+    if (recvcount == 0)
+        return MPI_SUCCESS;
+    if (hipGetDevice(&cur) == hipSuccess && cur != c->device)
+        (void) hipSetDevice(c->device);
+    s = hip_stream ? (hipStream_t) hip_stream : c->stream;
+    esz = MPIR_Hip_elem_size(elem);
+    nb = (size_t) recvcount * esz;
+    p = c->size;
+    src = sendbuf == MPI_IN_PLACE ? (const char *) recvbuf : (const char *) sendbuf;
+
+    if (want_rccl(c, algorithm, elem, opidx, &nt, &no)) {
+        ncclResult_t r;
+        /* NCCL's in-place form is recvbuff == sendbuff + rank * recvcount */
+        void *dst = sendbuf == MPI_IN_PLACE ? (char *) recvbuf + (size_t) c->rank * nb : recvbuf;
+        r = rccl.ReduceScatter(src, dst, (size_t) recvcount, nt, no, c->nccl, s);
+        if (r != ncclSuccess) {
+            MPIR_Err_set_detail("ncclReduceScatter: %s", rccl.GetErrorString ? rccl.GetErrorString(r) : "?");
+            rc = MPI_ERR_OTHER;
+            goto done;
+        }
+        if (sendbuf == MPI_IN_PLACE && c->rank)
+            HIPTRY(hipMemcpyAsync(recvbuf, dst, nb, hipMemcpyDeviceToDevice, s));
+        goto done_sync;
+    }
+
+    /* ---- reference order (reduce_scatter_block_intra_pairwise.c:97-134):
+     * block r = ((x_r + x_{r-1}) + x_{r-2}) + ...; y_i = block r from rank r - i */
+    if (comm_scratch(c, (size_t) (p > 1 ? p - 1 : 1) * nb + 256, &scr)) {
+        MPIR_Err_set_detail("%s: scratch allocation failed", fc);
+        rc = MPI_ERR_NO_MEM;
+        goto done;
+    }
+    for (i = 1; i < p; i++) {
+        int dst = (c->rank + i) % p, from = (c->rank - i + p) % p;
+        sends[i - 1].buf = (void *) (src + (size_t) dst * nb);
+        sends[i - 1].bytes = nb;
+        sends[i - 1].peer = dst;
+        recvs[i - 1].buf = scr + (size_t) (i - 1) * nb;
+        recvs[i - 1].bytes = nb;
+        recvs[i - 1].peer = from;
+    }
+    if (p > 1)
+        TRY(group_exchange(c, sends, p - 1, recvs, p - 1, s));
+    ys[0] = src + (size_t) c->rank * nb;
+    for (i = 1; i < p; i++)
+        ys[i] = scr + (size_t) (i - 1) * nb;
+    rc = MPIR_Hip_combine(ys, p, recvbuf, (uint64_t) recvcount, opidx, elem, MPIR_HIP_ORDER_CHAIN, s, 0);
+    if (rc) {
+        MPIR_Op_report_hip_error(fc, rc);
+        rc = MPI_ERR_OTHER;
+        goto done;
+    }
+
+  done_sync:
+    if (rc == MPI_SUCCESS && !hip_stream)
+        HIPTRY(hipStreamSynchronize(s));
+  done:
+    if (cur != c->device)
+        (void) hipSetDevice(cur);
+    return rc ? MPIR_Err_return(fc, rc) : MPI_SUCCESS;
+}

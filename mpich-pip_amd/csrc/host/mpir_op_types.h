@@ -53,6 +53,10 @@ int *MPIR_Op_errno_ptr(void);
 /* record a HIP runtime failure inside an op kernel (sets op_errno) */
 void MPIR_Op_report_hip_error(const char *opname, int hip_rc);
 
+/* the MPI-level error exit shared by every entry point: applies the
+ * MPIX_Reduce_local errhandler (fatal by default) and returns the class */
+int MPIR_Err_return(const char *fcname, int mpi_errno);
+
 /* last error detail text for this thread (for MPI_Error_string) */
 const char *MPIR_Err_last_detail(void);
 void MPIR_Err_set_detail(const char *fmt, ...);

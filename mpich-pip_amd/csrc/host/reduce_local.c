@@ -145,7 +145,7 @@ int MPIX_Reduce_local_get_errhandler(MPI_Errhandler * errhandler)
 }
 
 /* MPIR_Err_return_comm(NULL, fcname, errcode) (errutil.c:238) */
-static int err_return(const char *fcname, int mpi_errno)
+int MPIR_Err_return(const char *fcname, int mpi_errno)
 {
     if (reduce_local_errhandler == MPI_ERRORS_ARE_FATAL) {
         fprintf(stderr, "Fatal error in %s: %s, error stack:\n%s: %s\n", fcname,
@@ -155,6 +155,8 @@ static int err_return(const char *fcname, int mpi_errno)
     }
     return mpi_errno;
 }
+
+#define err_return MPIR_Err_return
 
 static int alias_check_enabled(void)
 {

@@ -108,6 +108,10 @@ EXPORTED_SYMBOLS = [
     "MPI_Error_class", "MPI_Error_string",
     "MPIX_Reduce_local_stream", "MPIX_Reduce_local_set_errhandler", "MPIX_Reduce_local_get_errhandler",
     "MPIX_Reduce_local_multi", "MPIR_Hip_combine",
+    # device collectives (include/mpix_hip_coll.h)
+    "MPIX_Hip_comm_get_unique_id", "MPIX_Hip_comm_create", "MPIX_Hip_comm_create_loopback",
+    "MPIX_Hip_comm_free", "MPIX_Hip_comm_rank", "MPIX_Hip_comm_size",
+    "MPIX_Allreduce_hip", "MPIX_Reduce_scatter_block_hip",
     # the HIP shim (include/mpir_hip_reduce.h)
     "MPIR_Hip_reduce", "MPIR_Hip_elem_size", "MPIR_Hip_has_kernel", "MPIR_Hip_is_device_ptr",
     "MPIR_Hip_memcpy", "MPIR_Hip_error_string", "MPIR_Hip_device_count",
@@ -138,6 +142,18 @@ def load(path: str | None = None) -> ctypes.CDLL:
     lib.MPIX_Reduce_local_stream.restype = i32
     lib.MPIX_Reduce_local_multi.argtypes = [ctypes.POINTER(vp), i32, vp, i32, i32, i32, i32, vp]
     lib.MPIX_Reduce_local_multi.restype = i32
+    lib.MPIX_Hip_comm_get_unique_id.argtypes = [vp]
+    lib.MPIX_Hip_comm_get_unique_id.restype = i32
+    lib.MPIX_Hip_comm_create.argtypes = [vp, i32, i32, ctypes.POINTER(vp)]
+    lib.MPIX_Hip_comm_create.restype = i32
+    lib.MPIX_Hip_comm_create_loopback.argtypes = [i32, ctypes.POINTER(vp)]
+    lib.MPIX_Hip_comm_create_loopback.restype = i32
+    lib.MPIX_Hip_comm_free.argtypes = [ctypes.POINTER(vp)]
+    lib.MPIX_Hip_comm_free.restype = i32
+    for name in ("MPIX_Allreduce_hip", "MPIX_Reduce_scatter_block_hip"):
+        f = getattr(lib, name)
+        f.argtypes = [vp, vp, i32, i32, i32, vp, i32, vp]
+        f.restype = i32
     lib.MPIX_Reduce_local_set_errhandler.argtypes = [i32]
     lib.MPIX_Reduce_local_set_errhandler.restype = i32
     lib.MPI_Op_create.argtypes = [MPI_User_function, i32, ctypes.POINTER(i32)]
@@ -190,6 +206,39 @@ def reduce_local_multi(inbufs, outbuf: int, count: int, datatype: int, op: int, 
     arr = (ctypes.c_void_p * len(inbufs))(*inbufs)
     return load().MPIX_Reduce_local_multi(arr, len(inbufs), ctypes.c_void_p(outbuf), count, datatype, op, order,
                                           ctypes.c_void_p(stream or None))
+
+
+MPIX_HIP_ALG_AUTO = 0
+MPIX_HIP_ALG_REFERENCE_ORDER = 1
+MPIX_HIP_ALG_RCCL = 2
+MPI_IN_PLACE = ctypes.c_void_p(-1 & 0xFFFFFFFFFFFFFFFF).value
+
+
+def comm_create_loopback(size: int):
+    """`size` in-process virtual ranks on the current device (one thread each)."""
+    arr = (ctypes.c_void_p * size)()
+    rc = load().MPIX_Hip_comm_create_loopback(size, arr)
+    if rc:
+        raise RuntimeError(error_string(rc))
+    return [arr[i] for i in range(size)]
+
+
+def comm_free(comm) -> int:
+    c = ctypes.c_void_p(comm)
+    return load().MPIX_Hip_comm_free(ctypes.byref(c))
+
+
+def allreduce(sendbuf, recvbuf: int, count: int, datatype: int, op: int, comm, algorithm: int = 0,
+              stream: int = 0) -> int:
+    return load().MPIX_Allreduce_hip(ctypes.c_void_p(sendbuf), ctypes.c_void_p(recvbuf), count, datatype, op,
+                                     ctypes.c_void_p(comm), algorithm, ctypes.c_void_p(stream or None))
+
+
+def reduce_scatter_block(sendbuf, recvbuf: int, recvcount: int, datatype: int, op: int, comm,
+                         algorithm: int = 0, stream: int = 0) -> int:
+    return load().MPIX_Reduce_scatter_block_hip(ctypes.c_void_p(sendbuf), ctypes.c_void_p(recvbuf), recvcount,
+                                                datatype, op, ctypes.c_void_p(comm), algorithm,
+                                                ctypes.c_void_p(stream or None))
 
 
 def reduce_local_stream(inbuf: int, inoutbuf: int, count: int, datatype: int, op: int, stream: int = 0) -> int:

@@ -1,0 +1,133 @@
+"""Device collectives (MPIX_Allreduce_hip, MPIX_Reduce_scatter_block_hip) on one GPU.
+
+The loopback communicator runs p virtual ranks in this process (one host
+thread each, transfers are device copies), so the complete reference-order
+algorithm -- pre-fold, all-to-all of blocks, fused tree/chain combine,
+allgather -- runs end to end on one MI355X.  The RCCL communicator differs
+only in its transport (grouped ncclSend/ncclRecv) and needs one GPU per rank.
+Expected bytes: oracle/schedules.py, the reference schedules run step by step
+on the CPU oracle.  Bit-exact (complex NaN payloads excepted).
+"""
+import threading
+
+import numpy as np
+import pytest
+
+import _types as T
+from test_parity_gpu import same
+
+pytestmark = pytest.mark.gpu
+
+
+def run_ranks(fn, p, timeout=120):
+    errs = [None] * p
+
+    def wrap(r):
+        try:
+            fn(r)
+        except BaseException as e:  # noqa: BLE001
+            errs[r] = e
+
+    ths = [threading.Thread(target=wrap, args=(r,), daemon=True) for r in range(p)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join(timeout)
+        if t.is_alive():
+            pytest.fail("collective did not complete (deadlock?)")
+    for e in errs:
+        if e is not None:
+            raise e
+
+
+CASES = [("MPI_FLOAT", "MPI_SUM"), ("MPIX_C_FLOAT16", "MPI_SUM"), ("MPI_INT", "MPI_SUM"),
+         ("MPI_DOUBLE", "MPI_MAX"), ("MPI_UNSIGNED_CHAR", "MPI_BXOR"), ("MPI_C_DOUBLE_COMPLEX", "MPI_SUM"),
+         ("MPI_DOUBLE_INT", "MPI_MAXLOC")]
+
+
+@pytest.mark.parametrize("t,op", CASES, ids=[f"{t}-{o}" for t, o in CASES])
+@pytest.mark.parametrize("p", [1, 2, 3, 4, 5, 8])
+@pytest.mark.parametrize("inplace", [False, True])
+def test_allreduce_reference_order(mpi, orc, cuda, t, op, p, inplace):
+    from oracle import schedules as S
+    torch = cuda
+    esz = T.elem_size(t)
+    comms = mpi.comm_create_loopback(p)
+    try:
+        for count, seed in ((1003, p), (3, 11), ((1 << 19) + 3, 5 * p)):
+            rng = np.random.default_rng(seed)
+            xs = [T.to_bytes(T.gen(t, count, rng, op)) for _ in range(p)]
+            if p > 1:
+                want = S.allreduce_smp(xs, count, esz, mpi.DATATYPES[t], mpi.OPS[op])
+            else:
+                want = xs[0]
+            send = [torch.from_numpy(x.copy()).cuda() for x in xs]
+            recv = [s.clone() if inplace else torch.zeros_like(s) for s in send]
+            torch.cuda.synchronize()
+
+            def rank(r):
+                sb = mpi.MPI_IN_PLACE if inplace else send[r].data_ptr()
+                rc = mpi.allreduce(sb, recv[r].data_ptr(), count, mpi.DATATYPES[t], mpi.OPS[op], comms[r],
+                                   mpi.MPIX_HIP_ALG_REFERENCE_ORDER)
+                assert rc == 0, mpi.error_string(rc)
+
+            run_ranks(rank, p)
+            torch.cuda.synchronize()
+            for r in range(p):
+                got = recv[r].cpu().numpy()
+                assert same(got, want, t), f"rank {r} count {count}: {np.count_nonzero(got != want)} bytes differ"
+    finally:
+        for c in comms:
+            mpi.comm_free(c)
+
+
+@pytest.mark.parametrize("t,op", [("MPIX_C_FLOAT16", "MPI_SUM"), ("MPI_FLOAT", "MPI_SUM"), ("MPI_INT64_T", "MPI_PROD"),
+                                  ("MPI_UNSIGNED", "MPI_BAND"), ("MPI_FLOAT", "MPI_MIN")])
+@pytest.mark.parametrize("p", [1, 2, 3, 8])
+@pytest.mark.parametrize("inplace", [False, True])
+def test_reduce_scatter_block_reference_order(mpi, orc, cuda, t, op, p, inplace):
+    from oracle import schedules as S
+    torch = cuda
+    esz = T.elem_size(t)
+    comms = mpi.comm_create_loopback(p)
+    try:
+        for recvcount, seed in ((2053, p), ((1 << 18) + 1, 3 * p)):
+            rng = np.random.default_rng(seed)
+            xs = [T.to_bytes(T.gen(t, recvcount * p, rng, op)) for _ in range(p)]
+            want = S.reduce_scatter_block_pairwise(xs, recvcount, esz, mpi.DATATYPES[t], mpi.OPS[op])
+            send = [torch.from_numpy(x.copy()).cuda() for x in xs]
+            recv = [s.clone() if inplace else torch.zeros(recvcount * esz, dtype=torch.uint8, device="cuda")
+                    for s in send]
+            torch.cuda.synchronize()
+
+            def rank(r):
+                sb = mpi.MPI_IN_PLACE if inplace else send[r].data_ptr()
+                rc = mpi.reduce_scatter_block(sb, recv[r].data_ptr(), recvcount, mpi.DATATYPES[t], mpi.OPS[op],
+                                              comms[r], mpi.MPIX_HIP_ALG_REFERENCE_ORDER)
+                assert rc == 0, mpi.error_string(rc)
+
+            run_ranks(rank, p)
+            torch.cuda.synchronize()
+            for r in range(p):
+                got = recv[r][:recvcount * esz].cpu().numpy()
+                assert same(got, want[r], t), f"rank {r}"
+    finally:
+        for c in comms:
+            mpi.comm_free(c)
+
+
+def test_collective_validation(mpi, cuda):
+    torch = cuda
+    comms = mpi.comm_create_loopback(1)
+    a = torch.zeros(16, device="cuda")
+    b = torch.zeros(16, device="cuda")
+    try:
+        assert mpi.allreduce(a.data_ptr(), b.data_ptr(), 16, mpi.MPI_FLOAT, mpi.MPI_LAND, comms[0]) == mpi.MPI_ERR_OP
+        assert mpi.allreduce(a.data_ptr(), a.data_ptr(), 16, mpi.MPI_FLOAT, mpi.MPI_SUM, comms[0]) == mpi.MPI_ERR_BUFFER
+        assert mpi.allreduce(a.data_ptr(), b.data_ptr(), -1, mpi.MPI_FLOAT, mpi.MPI_SUM, comms[0]) == mpi.MPI_ERR_COUNT
+        assert mpi.allreduce(a.data_ptr(), b.data_ptr(), 16, mpi.MPI_FLOAT, mpi.MPI_REPLACE, comms[0]) == mpi.MPI_ERR_OP
+        assert mpi.reduce_scatter_block(a.data_ptr(), b.data_ptr(), 16, mpi.MPI_BYTE, mpi.MPI_SUM,
+                                        comms[0]) == mpi.MPI_ERR_OP
+        assert mpi.allreduce(a.data_ptr(), b.data_ptr(), 0, mpi.MPI_FLOAT, mpi.MPI_SUM, comms[0]) == 0
+    finally:
+        mpi.comm_free(comms[0])
