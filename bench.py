@@ -57,6 +57,8 @@ def parse():
     ap.add_argument("--no-extras", action="store_true", help="only the timed MPI_Reduce_local loop")
     ap.add_argument("--cpu-threads", type=int, default=0, help="cpu_baseline threads (0 = min(16, affinity))")
     ap.add_argument("--cpu-iters", type=int, default=8)
+    ap.add_argument("--collectives", choices=["auto", "on", "off"], default="auto",
+                    help="configs 4-5 via bench_coll.py in isolated child processes (auto: when N > 1)")
     return ap.parse_args()
 
 
@@ -74,6 +76,31 @@ def time_steps(step, k: int, w: int, sync, barrier, max_over_ranks) -> float:
     t1 = time.perf_counter()
     barrier()
     return max_over_ranks(t1 - t0)
+
+
+def run_collectives_child(rank: int, world: int, local: int, barrier, timeout: float = 420.0):
+    """Configs 4-5 (Allreduce fp32 256 MiB, Reduce_scatter_block fp16 1 GiB) in a
+    child process per rank with its own RCCL communicator, so a failure there
+    cannot take this process's measurement down: the child is killed after
+    `timeout` seconds and the error is reported instead."""
+    import subprocess
+    barrier()
+    env = dict(os.environ, RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(local),
+               COLL_STORE_PORT=str(int(os.environ.get("MASTER_PORT", "29500")) + 101))
+    p = subprocess.Popen([sys.executable, os.path.join(ROOT, "bench_coll.py")], env=env,
+                         stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, start_new_session=True)
+    try:
+        so, se = p.communicate(timeout=timeout)
+    except subprocess.TimeoutExpired:
+        os.killpg(p.pid, 9)
+        p.communicate()
+        return {"error": f"timeout after {timeout:.0f} s"}
+    if p.returncode != 0:
+        return {"error": f"exit {p.returncode}", "stderr_tail": se.strip().splitlines()[-3:]}
+    lines = [ln for ln in so.splitlines() if ln.startswith("{")]
+    if rank == 0:
+        return json.loads(lines[-1]) if lines else {"error": "no output"}
+    return {}
 
 
 def load_traffic(count_bytes: int):
@@ -218,6 +245,11 @@ def main():
                                  "ms_per_step": round(dth / hk * 1e3, 3),
                                  "note": "pinned host in/inout: H2D x2 + kernel + D2H per 64 MiB chunk"}
         del ha, hb
+
+    if args.collectives == "on" or (args.collectives == "auto" and world > 1 and not args.no_extras):
+        coll = run_collectives_child(rank, world, local, barrier)
+        if rank == 0:
+            out["collectives"] = coll
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         import oracle

@@ -1,0 +1,164 @@
+#!/usr/bin/env python3
+"""Config 4 / 5 collectives on N GPUs, one process per GPU.
+
+    torchrun --nproc-per-node N --master-addr 127.0.0.1 bench_coll.py [--steps K]
+
+(bench.py runs this automatically, as isolated child processes, when it is
+launched with WORLD_SIZE > 1; its results land in bench.py's JSON line under
+"collectives".)
+
+Per rank: builds an RCCL communicator through the C ABI (MPIX_Hip_comm_create;
+unique id exchanged over a TCPStore on 127.0.0.1), then
+  1. parity on the real xGMI transport: a reference-order MPIX_Allreduce_hip
+     (fp32 SUM) and MPIX_Reduce_scatter_block_hip (fp16 SUM) on deterministic
+     per-rank inputs, checked bit for bit against oracle/schedules.py (the
+     reference schedules run step by step on the CPU oracle);
+  2. timing, config 4: MPI_Allreduce fp32 SUM, 256 MiB (67,108,864 floats);
+     config 5: MPI_Reduce_scatter_block fp16 SUM, 1 GiB sendbuf per rank
+     (recvcount 2^29 / N).  Both algorithms (RCCL, reference order); K timed
+     calls between a barrier and a device sync, max over ranks.
+Reports bus bandwidth the RCCL-tests way: allreduce 2(N-1)/N * bytes / t,
+reduce-scatter (N-1)/N * sendbytes / t.
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import datetime
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "mpich-pip_amd"))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--ar-mib", type=int, default=256)
+    ap.add_argument("--rs-mib", type=int, default=1024)
+    ap.add_argument("--store-port", type=int, default=int(os.environ.get("COLL_STORE_PORT", "29611")))
+    args = ap.parse_args()
+
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    import mpich_pip_amd as m
+    import _types as T
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    lib = m.load()
+    lib.MPIX_Reduce_local_set_errhandler(m.MPI_ERRORS_RETURN)
+
+    store = dist.TCPStore("127.0.0.1", args.store_port, world, rank == 0,
+                          timeout=datetime.timedelta(seconds=120))
+    if rank == 0:
+        uid = ctypes.create_string_buffer(128)
+        assert lib.MPIX_Hip_comm_get_unique_id(uid) == 0
+        store.set("mpix_uid", uid.raw)
+    raw = store.get("mpix_uid")
+    comm = ctypes.c_void_p()
+    rc = lib.MPIX_Hip_comm_create(ctypes.c_char_p(raw), world, rank, ctypes.byref(comm))
+    if rc:
+        raise RuntimeError(m.error_string(rc))
+    C = comm.value
+    F32, F16, SUM, MAX = m.MPI_FLOAT, m.MPIX_C_FLOAT16, m.MPI_SUM, m.MPI_MAX
+    REF, RCCL = m.MPIX_HIP_ALG_REFERENCE_ORDER, m.MPIX_HIP_ALG_RCCL
+
+    scratch = torch.zeros(1, dtype=torch.float64, device="cuda")
+
+    def barrier():
+        torch.cuda.synchronize()
+        assert m.allreduce(m.MPI_IN_PLACE, scratch.data_ptr(), 1, m.MPI_DOUBLE, SUM, C, RCCL) == 0
+
+    def max_over_ranks(x):
+        t = torch.tensor([x], dtype=torch.float64, device="cuda")
+        assert m.allreduce(m.MPI_IN_PLACE, t.data_ptr(), 1, m.MPI_DOUBLE, MAX, C, RCCL) == 0
+        return float(t.item())
+
+    out = {"n_ranks": world}
+
+    # ---- 1. parity over the real transport (small, deterministic inputs)
+    from oracle import schedules as S
+    n = (1 << 16) + 3
+    xs = [T.to_bytes(T.gen("MPI_FLOAT", n, np.random.default_rng(77 + r))) for r in range(world)]
+    want = S.allreduce_smp(xs, n, 4, F32, SUM) if world > 1 else xs[0]
+    send = torch.from_numpy(xs[rank].copy()).cuda()
+    recv = torch.zeros_like(send)
+    torch.cuda.synchronize()
+    assert m.allreduce(send.data_ptr(), recv.data_ptr(), n, F32, SUM, C, REF) == 0
+    ok_ar = bool(np.array_equal(recv.cpu().numpy(), want))
+    rcount = 4099
+    hs = [T.to_bytes(T.gen("MPIX_C_FLOAT16", rcount * world, np.random.default_rng(91 + r))) for r in range(world)]
+    want_rs = S.reduce_scatter_block_pairwise(hs, rcount, 2, F16, SUM)[rank]
+    hsend = torch.from_numpy(hs[rank].copy()).cuda()
+    hrecv = torch.zeros(rcount * 2, dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
+    assert m.reduce_scatter_block(hsend.data_ptr(), hrecv.data_ptr(), rcount, F16, SUM, C, REF) == 0
+    ok_rs = bool(np.array_equal(hrecv.cpu().numpy(), want_rs))
+    flags = torch.tensor([float(ok_ar), float(ok_rs)], dtype=torch.float64, device="cuda")
+    assert m.allreduce(m.MPI_IN_PLACE, flags.data_ptr(), 2, m.MPI_DOUBLE, m.MPI_MIN, C, RCCL) == 0
+    out["parity_reference_order"] = {"allreduce_fp32_sum_bitexact": bool(flags[0].item() == 1.0),
+                                     "reduce_scatter_block_fp16_sum_bitexact": bool(flags[1].item() == 1.0),
+                                     "oracle": "oracle/schedules.py (reference schedules on the CPU oracle)"}
+
+    # ---- 2. timing
+    def timed(fn):
+        for _ in range(args.warmup):
+            fn()
+        barrier()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            fn()
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        return max_over_ranks(dt) / args.steps
+
+    count = args.ar_mib * (1 << 20) // 4
+    a = torch.rand(count, device="cuda") * 2 - 1
+    b = torch.empty_like(a)
+    def ar(alg):
+        rc = m.allreduce(a.data_ptr(), b.data_ptr(), count, F32, SUM, C, alg, 0)
+        if rc:
+            raise RuntimeError(m.error_string(rc))
+
+    def rs(alg):
+        rc = m.reduce_scatter_block(hs_.data_ptr(), hr_.data_ptr(), rc_, F16, SUM, C, alg, 0)
+        if rc:
+            raise RuntimeError(m.error_string(rc))
+
+    res = {}
+    for name, alg in (("rccl", RCCL), ("reference_order", REF)):
+        t = timed(lambda: ar(alg))
+        nbytes = count * 4
+        res[name] = {"ms": round(t * 1e3, 3), "algbw_GBps": round(nbytes / t / 1e9, 1),
+                     "busbw_GBps": round(2 * (world - 1) / world * nbytes / t / 1e9, 1)}
+    out["config4_allreduce_fp32_sum_256MiB"] = res
+    del a, b
+    torch.cuda.empty_cache()
+
+    total = args.rs_mib * (1 << 20) // 2
+    rc_ = total // world
+    hs_ = (torch.rand(rc_ * world, device="cuda") - 0.5).half()
+    hr_ = torch.empty(rc_, dtype=torch.float16, device="cuda")
+    res = {}
+    for name, alg in (("rccl", RCCL), ("reference_order", REF)):
+        t = timed(lambda: rs(alg))
+        sb = rc_ * world * 2
+        res[name] = {"ms": round(t * 1e3, 3), "busbw_GBps": round((world - 1) / world * sb / t / 1e9, 1)}
+    out["config5_reduce_scatter_block_fp16_sum_1GiB"] = res
+    m.comm_free(C)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()
