@@ -58,9 +58,26 @@ __device__ __forceinline__ u32x4 combine16(u32x4 a, u32x4 b) {
     Pack16<T> pa = __builtin_bit_cast(Pack16<T>, a);
     Pack16<T> pb = __builtin_bit_cast(Pack16<T>, b);
     Op op;
+    if constexpr (nan_fast<Op, T>::value) {
+        // plain IEEE arithmetic (packed where the ISA has it); the x86 NaN
+        // rule runs only for lanes whose vector produced a NaN
+        Pack16<T> pr;
+        bool bad = false;
 #pragma unroll
-    for (int k = 0; k < (int)(16 / sizeof(T)); ++k) pa.e[k] = op(pa.e[k], pb.e[k]);
-    return __builtin_bit_cast(u32x4, pa);
+        for (int k = 0; k < (int)(16 / sizeof(T)); ++k) {
+            pr.e[k] = Op::raw(pa.e[k], pb.e[k]);
+            bad |= isnan_(pr.e[k]);
+        }
+        if (__builtin_expect(bad, 0)) {
+#pragma unroll
+            for (int k = 0; k < (int)(16 / sizeof(T)); ++k) pr.e[k] = op(pa.e[k], pb.e[k]);
+        }
+        return __builtin_bit_cast(u32x4, pr);
+    } else {
+#pragma unroll
+        for (int k = 0; k < (int)(16 / sizeof(T)); ++k) pa.e[k] = op(pa.e[k], pb.e[k]);
+        return __builtin_bit_cast(u32x4, pa);
+    }
 }
 
 template <class Op, class T>
@@ -182,18 +199,41 @@ struct MultiArgs {
     int64_t head_off, tail_off;     // byte offsets of head / tail from the region starts
 };
 
-template <class Op, class T, int P, bool TREE>
+template <class Op, class T, int P, bool TREE, bool RAW = false>
 __device__ __forceinline__ void fold_elems(T (&v)[P]) {
     Op op;
     if constexpr (TREE) {
 #pragma unroll
         for (int step = 1; step < P; step *= 2)
 #pragma unroll
-            for (int j = 0; j < P; j += 2 * step) v[j] = op(v[j], v[j + step]);
+            for (int j = 0; j < P; j += 2 * step) {
+                if constexpr (RAW) v[j] = Op::raw(v[j], v[j + step]);
+                else v[j] = op(v[j], v[j + step]);
+            }
     } else {
 #pragma unroll
-        for (int j = 1; j < P; ++j) v[0] = op(v[0], v[j]);
+        for (int j = 1; j < P; ++j) {
+            if constexpr (RAW) v[0] = Op::raw(v[0], v[j]);
+            else v[0] = op(v[0], v[j]);
+        }
     }
+}
+
+// fold with the fast path: plain arithmetic, then the exact x86-rule fold only
+// if the result is NaN (a NaN anywhere in an add/mul tree reaches the root)
+template <class Op, class T, int P, bool TREE>
+__device__ __forceinline__ T fold_fast(const T (&v0)[P]) {
+    T v[P];
+#pragma unroll
+    for (int j = 0; j < P; ++j) v[j] = v0[j];
+    if constexpr (nan_fast<Op, T>::value) {
+        fold_elems<Op, T, P, TREE, true>(v);
+        if (__builtin_expect(!isnan_(v[0]), 1)) return v[0];
+#pragma unroll
+        for (int j = 0; j < P; ++j) v[j] = v0[j];
+    }
+    fold_elems<Op, T, P, TREE>(v);
+    return v[0];
 }
 
 template <class Op, class T, int P, bool TREE, int U>
@@ -223,8 +263,7 @@ __global__ __launch_bounds__(kThreads) void k_combine_multi(MultiArgs a) {
                 T v[P];
 #pragma unroll
                 for (int j = 0; j < P; ++j) v[j] = pk[j].e[k];
-                fold_elems<Op, T, P, TREE>(v);
-                res.e[k] = v[0];
+                res.e[k] = fold_fast<Op, T, P, TREE>(v);
             }
             __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, res), ro,
                                                    (u * kThreads + (int)threadIdx.x) * 16, 0, kCachePolicyNT);

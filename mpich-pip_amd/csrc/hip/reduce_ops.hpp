@@ -94,6 +94,11 @@ struct OpSum {
     __device__ __forceinline__ double operator()(double a, double b) const { return xadd(a, b); }
     __device__ __forceinline__ cf32 operator()(cf32 a, cf32 b) const { return cf32{xadd(a.re, b.re), xadd(a.im, b.im)}; }
     __device__ __forceinline__ cf64 operator()(cf64 a, cf64 b) const { return cf64{xadd(a.re, b.re), xadd(a.im, b.im)}; }
+    // fast path for real types: a NaN operand or an invalid operation always
+    // yields a NaN result, so the x86 rule only needs to run when the plain
+    // result is NaN (see combine16 / fold_elems)
+    static constexpr bool kNanFast = true;
+    template <class R> static __device__ __forceinline__ R raw(R a, R b) { return a + b; }
 };
 
 // C99 Annex G complex multiply (a + ib) * (c + id), as gcc emits it for
@@ -150,6 +155,21 @@ struct OpProd {
     __device__ __forceinline__ cf64 operator()(cf64 a, cf64 b) const {
         cf64 r; annexg_mul<double>(a.re, a.im, b.re, b.im, r.re, r.im); return r;
     }
+    static constexpr bool kNanFast = true;
+    template <class R> static __device__ __forceinline__ R raw(R a, R b) { return a * b; }
+};
+
+template <class Op, class = void> struct has_nan_fast { static constexpr bool value = false; };
+template <class Op> struct has_nan_fast<Op, decltype((void)Op::kNanFast, void())> {
+    static constexpr bool value = Op::kNanFast;
+};
+template <class T> struct is_real { static constexpr bool value = false; };
+template <> struct is_real<f16> { static constexpr bool value = true; };
+template <> struct is_real<float> { static constexpr bool value = true; };
+template <> struct is_real<double> { static constexpr bool value = true; };
+// ops whose real-type combine takes the plain-arithmetic fast path
+template <class Op, class T> struct nan_fast {
+    static constexpr bool value = has_nan_fast<Op>::value && is_real<T>::value;
 };
 
 // MPL_MAX(a,b) (((a) > (b)) ? (a) : (b)); a = inout, b = in

@@ -112,13 +112,17 @@ int main(int argc, char **argv) {
         CK(hipMemcpy(io[s], h.data(), bytes, hipMemcpyHostToDevice));
     }
     std::vector<Var> vs = {
-        {"SUM fp32 product", 4, &launch_reduce<OpSum, float>, {}},
+        {"SUM fp32", 4, &launch_reduce<OpSum, float>, {}},
         {"SUM fp32 plain add", 4, &launch_reduce<OpSumPlain, float>, {}},
-        {"SUM fp32 pipe grid 1024", 4, &launch_pipe<1024>, {}},
-        {"SUM fp32 pipe grid 2048", 4, &launch_pipe<2048>, {}},
-        {"SUM fp32 pipe grid 4096", 4, &launch_pipe<4096>, {}},
-        {"SUM fp32 two tiles/WG", 4, &launch_two, {}},
-        {"SUM fp32 product (again)", 4, &launch_reduce<OpSum, float>, {}},
+        {"SUM fp16", 2, &launch_reduce<OpSum, f16>, {}},
+        {"SUM fp64", 8, &launch_reduce<OpSum, double>, {}},
+        {"PROD fp32", 4, &launch_reduce<OpProd, float>, {}},
+        {"MAX fp32", 4, &launch_reduce<OpMax, float>, {}},
+        {"SUM int32", 4, &launch_reduce<OpSum, int32_t>, {}},
+        {"SUM cf32", 8, &launch_reduce<OpSum, cf32>, {}},
+        {"PROD cf64", 16, &launch_reduce<OpProd, cf64>, {}},
+        {"MAXLOC double_int", 16, &launch_reduce<OpMaxloc, pdoubleint>, {}},
+        {"SUM fp32 (again)", 4, &launch_reduce<OpSum, float>, {}},
     };
     hipStream_t st;
     CK(hipStreamCreate(&st));
@@ -138,7 +142,37 @@ int main(int argc, char **argv) {
             if (r >= 0) v.ms.push_back(ms);
         }
     }
+    // fused schedule combines: P = 8 operands of `bytes` each -> 1 output
+    struct MVar { std::string name; size_t esz; hipError_t (*fn)(const void *const *, void *, uint64_t, hipStream_t); std::vector<float> ms; };
+    std::vector<MVar> mvs = {
+        {"TREE8 SUM fp32 (config 4 combine)", 4, &launch_combine_p<OpSum, float, 8, true>, {}},
+        {"CHAIN8 SUM fp16 (config 5 combine)", 2, &launch_combine_p<OpSum, f16, 8, false>, {}},
+        {"CHAIN8 SUM fp32", 4, &launch_combine_p<OpSum, float, 8, false>, {}},
+    };
+    const int P = 8;
+    char *mins[P];
+    for (int j = 0; j < P; ++j) { CK(hipMalloc(&mins[j], bytes)); CK(hipMemcpy(mins[j], in[j % NS], bytes, hipMemcpyDeviceToDevice)); }
+    const void *mptr[P];
+    for (int j = 0; j < P; ++j) mptr[j] = mins[j];
+    for (int r = -2; r < rounds; ++r) {
+        for (auto &v : mvs) {
+            int s = slot++ % NS;
+            CK(hipEventRecord(e0, st));
+            CK(v.fn(mptr, io[s], bytes / v.esz, st));
+            CK(hipEventRecord(e1, st));
+            CK(hipEventSynchronize(e1));
+            float ms;
+            CK(hipEventElapsedTime(&ms, e0, e1));
+            if (r >= 0) v.ms.push_back(ms);
+        }
+    }
     printf("%zu MiB per operand, %d interleaved rounds\n", mib, rounds);
+    for (auto &v : mvs) {
+        std::sort(v.ms.begin(), v.ms.end());
+        double med = v.ms[v.ms.size() / 2];
+        double gbs = (P + 1.0) * bytes / (med * 1e-3) / 1e9;
+        printf("%-36s median %8.2f us -> %7.0f GB/s (9 x operand bytes) frac %.3f\n", v.name.c_str(), med * 1e3, gbs, gbs / 8000.0);
+    }
     for (auto &v : vs) {
         std::sort(v.ms.begin(), v.ms.end());
         double med = v.ms[v.ms.size() / 2], mn = v.ms[0];
