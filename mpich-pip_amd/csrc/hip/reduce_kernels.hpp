@@ -298,9 +298,8 @@ __global__ __launch_bounds__(kThreads) void k_combine_multi_elems(MultiArgs a, u
     }
 }
 
-template <class Op, class T, int P, bool TREE>
-hipError_t launch_combine_p(const void *const *ins, void *out_, uint64_t count, hipStream_t s) {
-    constexpr int U = P >= 8 ? 1 : (P >= 4 ? 2 : 4);
+template <class Op, class T, int P, bool TREE, int U>
+hipError_t launch_combine_pu(const void *const *ins, void *out_, uint64_t count, hipStream_t s) {
     constexpr uint32_t tile = kThreads * U * 16;
     char *out = static_cast<char *>(out_);
     const uintptr_t ao = reinterpret_cast<uintptr_t>(out);
@@ -335,6 +334,11 @@ hipError_t launch_combine_p(const void *const *ins, void *out_, uint64_t count, 
         hipLaunchKernelGGL((k_combine_multi_elems<Op, T, P, TREE>), dim3((unsigned)grid), dim3(kThreads), 0, s, a, count);
     }
     return hipGetLastError();
+}
+
+template <class Op, class T, int P, bool TREE>
+hipError_t launch_combine_p(const void *const *ins, void *out_, uint64_t count, hipStream_t s) {
+    return launch_combine_pu<Op, T, P, TREE, (P >= 8 ? 1 : (P >= 4 ? 2 : 4))>(ins, out_, count, s);
 }
 
 }  // namespace mpir_hip

@@ -307,3 +307,63 @@ def test_complex_special_pairs(mpi, orc, cuda, op, t):
     # the non-NaN part really is exercised: infinities from the Annex G recovery
     if op == "MPI_PROD":
         assert np.isinf(got.view(ft)).sum() > 100
+
+
+def test_maximum_count_int_max(mpi, cuda):
+    """count = INT_MAX (the reference's `int count` limit): 2 GiB of MPI_BYTE
+    BXOR and 8 GiB fp32 SUM per operand; checked on the device with torch
+    (XOR / IEEE add are exact elementwise, so torch's result is the oracle's)."""
+    torch = cuda
+    n = 2 ** 31 - 1
+    a = torch.randint(0, 256, (n + 1,), dtype=torch.uint8, device="cuda")[:n]
+    b = torch.randint(0, 256, (n + 1,), dtype=torch.uint8, device="cuda")[:n]
+    want = torch.bitwise_xor(a, b)
+    torch.cuda.synchronize()
+    assert mpi.reduce_local(b.data_ptr(), a.data_ptr(), n, mpi.MPI_BYTE, mpi.MPI_BXOR) == 0
+    assert torch.equal(a, want)
+    del a, b, want
+    torch.cuda.empty_cache()
+    x = torch.rand(n, device="cuda")
+    y = torch.rand(n, device="cuda")
+    want = x + y
+    torch.cuda.synchronize()
+    assert mpi.reduce_local(y.data_ptr(), x.data_ptr(), n, mpi.MPI_FLOAT, mpi.MPI_SUM) == 0
+    assert torch.equal(x.view(torch.int32), want.view(torch.int32))
+    # the last elements (tail of the final tile) really were combined
+    assert torch.equal(x[-5:].view(torch.int32), want[-5:].view(torch.int32))
+
+
+def test_concurrent_host_threads(mpi, orc, cuda):
+    """MPIR_Reduce_local is reentrant (per-thread op_errno, stream, wait flag):
+    8 host threads reduce their own buffers at once."""
+    import threading
+    torch = cuda
+    n = (1 << 20) + 11
+    rng = np.random.default_rng(3)
+    data = []
+    for i in range(8):
+        a = T.to_bytes(T.gen("MPI_DOUBLE", n, rng))
+        b = T.to_bytes(T.gen("MPI_DOUBLE", n, rng))
+        w = a.copy()
+        orc.reduce_local(b.copy(), w, n, mpi.MPI_DOUBLE, mpi.MPI_SUM)
+        data.append((torch.from_numpy(a).cuda(), torch.from_numpy(b).cuda(), w))
+    torch.cuda.synchronize()
+    errs = []
+
+    def work(i):
+        da, db, _ = data[i]
+        rc = mpi.reduce_local(db.data_ptr(), da.data_ptr(), n, mpi.MPI_DOUBLE, mpi.MPI_SUM)
+        if rc:
+            errs.append(rc)
+        # an invalid call on the same thread must not disturb the others
+        if mpi.reduce_local(db.data_ptr(), da.data_ptr(), n, mpi.MPI_DOUBLE, mpi.MPI_BAND) != mpi.MPI_ERR_OP:
+            errs.append("band")
+
+    ths = [threading.Thread(target=work, args=(i,)) for i in range(8)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join(120)
+    assert not errs
+    for da, db, w in data:
+        assert np.array_equal(da.cpu().numpy(), w)

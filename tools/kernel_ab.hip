@@ -89,6 +89,11 @@ hipError_t launch_two(const void *in, void *io, uint64_t count, hipStream_t s) {
     return hipGetLastError();
 }
 
+// plain adds with no NaN rule, for the A/B of the fused tree's fast path
+struct OpSumPlainM {
+    __device__ __forceinline__ float operator()(float a, float b) const { return a + b; }
+};
+
 struct Var {
     std::string name;
     size_t esz;
@@ -145,9 +150,15 @@ int main(int argc, char **argv) {
     // fused schedule combines: P = 8 operands of `bytes` each -> 1 output
     struct MVar { std::string name; size_t esz; hipError_t (*fn)(const void *const *, void *, uint64_t, hipStream_t); std::vector<float> ms; };
     std::vector<MVar> mvs = {
-        {"TREE8 SUM fp32 (config 4 combine)", 4, &launch_combine_p<OpSum, float, 8, true>, {}},
-        {"CHAIN8 SUM fp16 (config 5 combine)", 2, &launch_combine_p<OpSum, f16, 8, false>, {}},
-        {"CHAIN8 SUM fp32", 4, &launch_combine_p<OpSum, float, 8, false>, {}},
+        {"TREE8 SUM fp32 U1 (product)", 4, &launch_combine_p<OpSum, float, 8, true>, {}},
+        {"TREE8 SUM fp32 U2", 4, &launch_combine_pu<OpSum, float, 8, true, 2>, {}},
+        {"TREE8 SUM fp32 U4", 4, &launch_combine_pu<OpSum, float, 8, true, 4>, {}},
+        {"TREE8 SUM fp32 U1 plain", 4, &launch_combine_pu<OpSumPlainM, float, 8, true, 1>, {}},
+        {"CHAIN8 SUM fp16 U1 (product)", 2, &launch_combine_p<OpSum, f16, 8, false>, {}},
+        {"CHAIN8 SUM fp16 U2", 2, &launch_combine_pu<OpSum, f16, 8, false, 2>, {}},
+        {"CHAIN8 SUM fp32 U1", 4, &launch_combine_p<OpSum, float, 8, false>, {}},
+        {"TREE4 SUM fp32 U2 (product)", 4, &launch_combine_p<OpSum, float, 4, true>, {}},
+        {"TREE2 SUM fp32 U4 (product)", 4, &launch_combine_p<OpSum, float, 2, true>, {}},
     };
     const int P = 8;
     char *mins[P];
@@ -170,8 +181,9 @@ int main(int argc, char **argv) {
     for (auto &v : mvs) {
         std::sort(v.ms.begin(), v.ms.end());
         double med = v.ms[v.ms.size() / 2];
-        double gbs = (P + 1.0) * bytes / (med * 1e-3) / 1e9;
-        printf("%-36s median %8.2f us -> %7.0f GB/s (9 x operand bytes) frac %.3f\n", v.name.c_str(), med * 1e3, gbs, gbs / 8000.0);
+        int pp = v.name.find("TREE4") != std::string::npos ? 4 : (v.name.find("TREE2") != std::string::npos ? 2 : 8);
+        double gbs = (pp + 1.0) * bytes / (med * 1e-3) / 1e9;
+        printf("%-36s median %8.2f us -> %7.0f GB/s ((P+1) x operand bytes) frac %.3f\n", v.name.c_str(), med * 1e3, gbs, gbs / 8000.0);
     }
     for (auto &v : vs) {
         std::sort(v.ms.begin(), v.ms.end());
