@@ -56,7 +56,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="only the timed MPI_Reduce_local loop")
     ap.add_argument("--cpu-threads", type=int, default=0, help="cpu_baseline threads (0 = min(16, affinity))")
-    ap.add_argument("--cpu-iters", type=int, default=8)
+    ap.add_argument("--cpu-iters", type=int, default=48)
     ap.add_argument("--collectives", choices=["auto", "on", "off"], default="auto",
                     help="configs 4-5 via bench_coll.py in isolated child processes (auto: when N > 1)")
     return ap.parse_args()
