@@ -1,0 +1,149 @@
+// sync_flag.hip -- cost of the synchronous-return protocol around one 256 MiB
+// fp32 SUM tile kernel (the MPI_Reduce_local hot path).
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -Iinclude -Impich-pip_amd/csrc/hip \
+//         -o tools/sync_flag tools/sync_flag.hip \
+//         -Lmpich-pip_amd/lib -lmpich_reduce_local -Wl,-rpath,$PWD/mpich-pip_amd/lib
+// Variants (per-call microseconds, 256 MiB and a 1-workgroup call):
+//   lib       MPI_Reduce_local (library as shipped)
+//   wv32      tile kernel + hipStreamWriteValue32(flag) + host spin
+//   evsync    tile kernel + hipEventRecord + hipEventSynchronize
+//   done_all  kernel signals completion itself: every lane __threadfence(),
+//             barrier, lane 0 counts the workgroup; the last one stores the
+//             flag (system scope); host spins
+//   done_t0   same, but only lane 0 fences (after the barrier)
+//   done_nf   same, no fence (lower bound; not a valid protocol)
+#include <hip/hip_runtime.h>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+#include "mpi_reduce_local.h"
+#include "reduce_kernels.hpp"
+
+using namespace mpir_hip;
+#define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP %s line %d\n", hipGetErrorString(e_), __LINE__); exit(2);} } while (0)
+
+static double now() { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); }
+
+template <int MODE>
+__global__ __launch_bounds__(kThreads) void k_tile_done(const char *in, char *io, uint64_t vbytes, unsigned *counter,
+                                                         unsigned *hflag, unsigned seq) {
+    const uint64_t base = (uint64_t)blockIdx.x * kTileBytes;
+    if (base < vbytes) {
+        const uint64_t left = vbytes - base;
+        const int nrec = (int)(left < kTileBytes ? left : kTileBytes);
+        __amdgpu_buffer_rsrc_t rin = __builtin_amdgcn_make_buffer_rsrc((void *)(in + base), 0, nrec, 0x00020000);
+        __amdgpu_buffer_rsrc_t rio = __builtin_amdgcn_make_buffer_rsrc((void *)(io + base), 0, nrec, 0x00020000);
+        u32x4 a[kVecPerLane], b[kVecPerLane];
+#pragma unroll
+        for (int u = 0; u < kVecPerLane; ++u) {
+            const int off = (u * kThreads + (int)threadIdx.x) * 16;
+            a[u] = __builtin_amdgcn_raw_buffer_load_b128(rio, off, 0, kCachePolicyNT);
+            b[u] = __builtin_amdgcn_raw_buffer_load_b128(rin, off, 0, kCachePolicyNT);
+        }
+#pragma unroll
+        for (int u = 0; u < kVecPerLane; ++u) {
+            const int off = (u * kThreads + (int)threadIdx.x) * 16;
+            __builtin_amdgcn_raw_buffer_store_b128(combine16<OpSum, float>(a[u], b[u]), rio, off, 0, kCachePolicyNT);
+        }
+    }
+    if constexpr (MODE == 1) __threadfence();
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        if constexpr (MODE == 2) __threadfence();
+        unsigned old = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (old == gridDim.x - 1) {
+            __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "");
+            __hip_atomic_store(hflag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
+}
+
+int main() {
+    MPIX_Reduce_local_set_errhandler(MPI_ERRORS_RETURN);
+    const size_t n = 64ull << 20;  // floats = 256 MiB
+    float *a[2], *b[2];
+    for (int i = 0; i < 2; ++i) {
+        CK(hipMalloc(&a[i], n * 4)); CK(hipMalloc(&b[i], n * 4));
+        CK(hipMemset(a[i], 0, n * 4)); CK(hipMemset(b[i], 0, n * 4));
+    }
+    unsigned *counter;
+    CK(hipMalloc(&counter, 64)); CK(hipMemset(counter, 0, 64));
+    volatile unsigned *flag;
+    CK(hipHostMalloc((void **)&flag, 64, hipHostMallocCoherent | hipHostMallocMapped));
+    *flag = 0;
+    hipStream_t s; CK(hipStreamCreate(&s));
+    hipEvent_t ev; CK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    CK(hipDeviceSynchronize());
+    unsigned seq = 0;
+    const int R = 5;  // interleaved rounds
+
+    auto run = [&](int v, size_t cnt, int k) -> double {
+        const uint64_t vb = cnt * 4;
+        const unsigned grid = (unsigned)((vb + kTileBytes - 1) / kTileBytes);
+        double t0 = now();
+        for (int i = 0; i < k; ++i) {
+            float *x = a[i & 1], *y = b[i & 1];
+            ++seq;
+            switch (v) {
+            case 0: if (MPI_Reduce_local(x, y, (int)cnt, MPI_FLOAT, MPI_SUM)) { printf("rc\n"); exit(1); } break;
+            case 1:
+                launch_reduce<OpSum, float>(x, y, cnt, s);
+                CK(hipStreamWriteValue32(s, (void *)flag, seq, 0));
+                while (*flag != seq) __builtin_ia32_pause();
+                break;
+            case 2:
+                launch_reduce<OpSum, float>(x, y, cnt, s);
+                CK(hipEventRecord(ev, s)); CK(hipEventSynchronize(ev));
+                break;
+            case 3: case 4: case 5:
+                if (v == 3) hipLaunchKernelGGL(k_tile_done<1>, dim3(grid), dim3(kThreads), 0, s, (const char *)x, (char *)y, vb, counter, (unsigned *)flag, seq);
+                if (v == 4) hipLaunchKernelGGL(k_tile_done<2>, dim3(grid), dim3(kThreads), 0, s, (const char *)x, (char *)y, vb, counter, (unsigned *)flag, seq);
+                if (v == 5) hipLaunchKernelGGL(k_tile_done<0>, dim3(grid), dim3(kThreads), 0, s, (const char *)x, (char *)y, vb, counter, (unsigned *)flag, seq);
+                while (*flag != seq) __builtin_ia32_pause();
+                break;
+            }
+        }
+        return (now() - t0) / k * 1e6;
+    };
+    const char *names[] = {"lib", "wv32", "evsync", "done_all", "done_t0", "done_nf"};
+    const size_t sizes[] = {4096, n};
+    for (size_t cnt : sizes) {
+        std::vector<double> best(6, 1e30), sum(6, 0);
+        for (int v = 0; v < 6; ++v) run(v, cnt, 5);
+        CK(hipStreamSynchronize(s));
+        for (int r = 0; r < R; ++r)
+            for (int v = 0; v < 6; ++v) {
+                double us = run(v, cnt, cnt > 100000 ? 40 : 400);
+                CK(hipStreamSynchronize(s));
+                best[v] = us < best[v] ? us : best[v];
+                sum[v] += us;
+            }
+        for (int v = 0; v < 6; ++v)
+            printf("count %9zu %-9s mean %8.2f us  best %8.2f us  %8.1f GiB/s(alg, best)\n", cnt, names[v], sum[v] / R, best[v],
+                   12.0 * cnt / (best[v] * 1e-6) / (1 << 30));
+    }
+    // correctness of the in-kernel completion: a = 1, b = 2 -> b = 3, checked right after the flag
+    std::vector<float> h(n);
+    for (int v = 3; v <= 4; ++v) {
+        for (size_t i = 0; i < n; ++i) h[i] = 1.0f;
+        CK(hipMemcpy(a[0], h.data(), n * 4, hipMemcpyHostToDevice));
+        for (size_t i = 0; i < n; ++i) h[i] = 2.0f;
+        CK(hipMemcpy(b[0], h.data(), n * 4, hipMemcpyHostToDevice));
+        CK(hipDeviceSynchronize());
+        ++seq;
+        const unsigned grid = (unsigned)(n * 4 / kTileBytes);
+        if (v == 3) hipLaunchKernelGGL(k_tile_done<1>, dim3(grid), dim3(kThreads), 0, s, (const char *)a[0], (char *)b[0], (uint64_t)n * 4, counter, (unsigned *)flag, seq);
+        else hipLaunchKernelGGL(k_tile_done<2>, dim3(grid), dim3(kThreads), 0, s, (const char *)a[0], (char *)b[0], (uint64_t)n * 4, counter, (unsigned *)flag, seq);
+        while (*flag != seq) __builtin_ia32_pause();
+        hipStream_t s2; CK(hipStreamCreateWithFlags(&s2, hipStreamNonBlocking));
+        CK(hipMemcpyAsync(h.data(), b[0], n * 4, hipMemcpyDeviceToHost, s2));
+        CK(hipStreamSynchronize(s2));
+        size_t bad = 0;
+        for (size_t i = 0; i < n; ++i) bad += h[i] != 3.0f;
+        printf("%s: %zu wrong elements read right after the flag\n", names[v], bad);
+        CK(hipStreamSynchronize(s));
+    }
+    return 0;
+}
