@@ -24,7 +24,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def header_symbols():
     names = set()
-    for h in ("mpi_reduce_local.h", "mpir_hip_reduce.h", "mpix_hip_coll.h"):
+    for h in ("mpi_reduce_local.h", "mpir_hip_reduce.h", "mpix_hip_coll.h", "mpi_pip.h"):
         src = open(os.path.join(ROOT, "include", h)).read()
         src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
         for m in re.finditer(r"^\s*(?:extern\s+)?[A-Za-z_][\w\s\*]*?\b((?:P?MPI[RX]?|MPI)_\w+)\s*(\(|\[)", src, re.M):
