@@ -103,6 +103,74 @@ def run_collectives_child(rank: int, world: int, local: int, barrier, timeout: f
     return {}
 
 
+def event_launch_us(launch, k: int, w: int, stream) -> float:
+    """Mean per-launch kernel time (us) from HIP events recorded on `stream`."""
+    import torch
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(k)]
+    for i in range(w):
+        launch(i)
+    for i, (e0, e1) in enumerate(evs):
+        e0.record(stream)
+        launch(w + i)
+        e1.record(stream)
+    stream.synchronize()
+    return sum(e0.elapsed_time(e1) for e0, e1 in evs) / k * 1e3
+
+
+def config3_sweep(m, lib, pairs, nbytes: int, stream, k: int = 10, w: int = 3):
+    """BASELINE config 3: {SUM, MAX, MIN, PROD} x {int32, int64, fp32, fp64} at 256 MiB
+    per operand, kernel roofline fraction per (op, type).  The resident pairs are
+    reinterpreted per type; PROD multiplies by an all-ones inbuf so repeated
+    in-place calls stay finite."""
+    import torch
+    types = [("int32", m.MPI_INT32_T, torch.int32), ("int64", m.MPI_INT64_T, torch.int64),
+             ("fp32", m.MPI_FLOAT, torch.float32), ("fp64", m.MPI_DOUBLE, torch.float64)]
+    ops = [("SUM", m.MPI_SUM), ("MAX", m.MPI_MAX), ("MIN", m.MPI_MIN), ("PROD", m.MPI_PROD)]
+    res = {op: {} for op, _ in ops}
+    for tname, dt, tt in types:
+        esz = torch.tensor([], dtype=tt).element_size()
+        count = nbytes // esz
+        ones = torch.ones(count, dtype=tt, device="cuda")
+        for oname, op in ops:
+            def launch(i):
+                a, b = pairs[i & 1]
+                pin = ones.data_ptr() if oname == "PROD" else b.data_ptr()
+                rc = lib.MPIX_Reduce_local_stream(pin, a.data_ptr(), count, dt, op, stream.cuda_stream)
+                assert rc == 0, m.error_string(rc)
+            with torch.cuda.stream(stream):
+                us = event_launch_us(launch, k, w, stream)
+            res[oname][tname] = round(3 * nbytes / (us * 1e-6) / HBM_PEAK_BPS, 4)
+        del ones
+    torch.cuda.empty_cache()
+    return {"unit": "fraction of 8.0 TB/s (algorithmic bytes / mean HIP-event launch time)",
+            "operand_MiB": nbytes // MIB, **res}
+
+
+def config2(m, lib, pairs, stream, k: int, w: int):
+    """BASELINE config 2: fp32 SUM, 64 MiB per operand.  Eight distinct 64 MiB
+    (inbuf, inoutbuf) windows of the resident buffers are rotated, 512 MiB of
+    footprint per cycle, so no call finds its operands in the 256 MB Infinity Cache."""
+    import torch
+    count = 16 * MIB
+    wins = [(a[j * count:(j + 1) * count], b[j * count:(j + 1) * count]) for a, b in pairs for j in range(4)]
+
+    def launch(i):
+        a, b = wins[i % len(wins)]
+        assert lib.MPIX_Reduce_local_stream(b.data_ptr(), a.data_ptr(), count, m.MPI_FLOAT, m.MPI_SUM,
+                                            stream.cuda_stream) == 0
+    with torch.cuda.stream(stream):
+        us = event_launch_us(launch, k, w, stream)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(k):
+        a, b = wins[i % len(wins)]
+        assert lib.MPI_Reduce_local(b.data_ptr(), a.data_ptr(), count, m.MPI_FLOAT, m.MPI_SUM) == 0
+    dt = time.perf_counter() - t0
+    alg = 3 * count * 4
+    return {"kernel_us": round(us, 2), "kernel_frac": round(alg / (us * 1e-6) / HBM_PEAK_BPS, 4),
+            "sync_api_GiBps": round(alg * k / dt / GIB, 1), "windows": len(wins)}
+
+
 def load_traffic(count_bytes: int):
     """Per-launch HBM bytes of the dominant kernel from the committed PMC summary."""
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
@@ -222,6 +290,11 @@ def main():
             "median_launch_us": round(ms[len(ms) // 2] * 1e3, 2),
             "p10_p90_us": [round(ms[len(ms) // 10] * 1e3, 2), round(ms[(len(ms) * 9) // 10] * 1e3, 2)],
         }
+
+        # ---- configs 2 and 3 (kernel time per launch, same event method)
+        out["config3_sweep"] = config3_sweep(m, lib, pairs, nbytes, s)
+        if nbytes >= 256 * MIB:
+            out["config2_64MiB"] = config2(m, lib, pairs, s, args.steps, args.warmup)
 
         # ---- stream-ordered API, back to back (what the library's schedules drive)
         def sstep(i):

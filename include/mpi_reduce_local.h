@@ -5,9 +5,9 @@
  * Every declaration here replaces the symbol of the same name in the
  * reference (pmodels/mpich-pip, MPICH 3.3).  Handle values, error classes and
  * calling conventions are identical to an x86-64 MPICH 3.3 build configured
- * with --disable-fortran --disable-cxx and without long double (MPICH's
- * MPID_NO_LONG_DOUBLE), so the existing collective schedules and the RMA
- * accumulate path can call these functions unchanged.
+ * with --disable-fortran --disable-cxx (long double included: the x87 80-bit
+ * format is computed in software on the GPU), so the existing collective
+ * schedules and the RMA accumulate path can call these functions unchanged.
  *
  * Reference interfaces replaced (file:line under the reference tree):
  *   MPI_Reduce_local / PMPI_Reduce_local  src/include/mpi.h.in:1359,
@@ -103,7 +103,7 @@ typedef void (MPI_User_function) (void *invec, void *inoutvec, int *len, MPI_Dat
 #define MPI_LONG_LONG           MPI_LONG_LONG_INT
 #define MPI_FLOAT               ((MPI_Datatype)0x4c00040a)
 #define MPI_DOUBLE              ((MPI_Datatype)0x4c00080b)
-#define MPI_LONG_DOUBLE         MPI_DATATYPE_NULL       /* MPID_NO_LONG_DOUBLE build (0x4c00100c otherwise) */
+#define MPI_LONG_DOUBLE         ((MPI_Datatype)0x4c00100c)   /* x87 80-bit in a 16-byte slot */
 #define MPI_BYTE                ((MPI_Datatype)0x4c00010d)
 #define MPI_WCHAR               ((MPI_Datatype)0x4c00040e)
 #define MPI_PACKED              ((MPI_Datatype)0x4c00010f)
@@ -116,7 +116,7 @@ typedef void (MPI_User_function) (void *invec, void *inoutvec, int *len, MPI_Dat
 #define MPI_DOUBLE_INT          ((MPI_Datatype)0x8c000001)
 #define MPI_LONG_INT            ((MPI_Datatype)0x8c000002)
 #define MPI_SHORT_INT           ((MPI_Datatype)0x8c000003)
-#define MPI_LONG_DOUBLE_INT     MPI_DATATYPE_NULL       /* 0x8c000004 with long double */
+#define MPI_LONG_DOUBLE_INT     ((MPI_Datatype)0x8c000004)   /* {long double; int}, 32 B */
 #define MPI_INT8_T              ((MPI_Datatype)0x4c000137)
 #define MPI_INT16_T             ((MPI_Datatype)0x4c000238)
 #define MPI_INT32_T             ((MPI_Datatype)0x4c000439)
@@ -129,7 +129,7 @@ typedef void (MPI_User_function) (void *invec, void *inoutvec, int *len, MPI_Dat
 #define MPI_C_FLOAT_COMPLEX     ((MPI_Datatype)0x4c000840)
 #define MPI_C_COMPLEX           MPI_C_FLOAT_COMPLEX
 #define MPI_C_DOUBLE_COMPLEX    ((MPI_Datatype)0x4c001041)
-#define MPI_C_LONG_DOUBLE_COMPLEX MPI_DATATYPE_NULL     /* 0x4c002042 with long double */
+#define MPI_C_LONG_DOUBLE_COMPLEX ((MPI_Datatype)0x4c002042) /* long double _Complex, 32 B */
 #define MPIX_C_FLOAT16          ((MPI_Datatype)0x4c000246)
 #define MPI_AINT                ((MPI_Datatype)0x4c000843)
 #define MPI_OFFSET              ((MPI_Datatype)0x4c000844)

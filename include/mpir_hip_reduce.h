@@ -45,6 +45,8 @@ enum MPIR_Hip_elem {
     MPIR_HIP_CF32, MPIR_HIP_CF64,                 /* C float/double _Complex */
     MPIR_HIP_P2INT, MPIR_HIP_PFLOATINT, MPIR_HIP_PLONGINT,
     MPIR_HIP_PSHORTINT, MPIR_HIP_PDOUBLEINT,      /* MAXLOC/MINLOC pairs */
+    MPIR_HIP_F80, MPIR_HIP_CF80,                  /* x87 long double (16 B slot), its _Complex */
+    MPIR_HIP_PLDOUBLEINT,                         /* MPI_LONG_DOUBLE_INT pair (32 B) */
     MPIR_HIP_NELEMS
 };
 

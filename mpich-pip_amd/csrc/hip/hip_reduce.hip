@@ -24,6 +24,8 @@ Entry g_table[MPIR_HIP_NOPS][MPIR_HIP_NELEMS];
 
 template <class Op, class T>
 void reg(int op, int elem) { g_table[op][elem].fn = &launch_reduce<Op, T>; }
+template <class Op, class T>
+void reg_wide(int op, int elem) { g_table[op][elem].fn = &launch_reduce_wide<Op, T>; }
 
 // Integer element classes and their device types.
 #define FOR_INTS(X) \
@@ -63,6 +65,17 @@ struct TableInit {
 #define X(E, T) reg<OpMaxloc, T>(MPIR_HIP_OP_MAXLOC, E); reg<OpMinloc, T>(MPIR_HIP_OP_MINLOC, E);
         FOR_PAIRS(X)
 #undef X
+        // long double: FLOATING_POINT (SUM, PROD, MAX, MIN, LXOR), its _Complex
+        // (SUM, PROD), MPI_LONG_DOUBLE_INT (MAXLOC, MINLOC) -- x87 in software
+        reg<OpSum, x80>(MPIR_HIP_OP_SUM, MPIR_HIP_F80);
+        reg<OpProd, x80>(MPIR_HIP_OP_PROD, MPIR_HIP_F80);
+        reg<OpMax, x80>(MPIR_HIP_OP_MAX, MPIR_HIP_F80);
+        reg<OpMin, x80>(MPIR_HIP_OP_MIN, MPIR_HIP_F80);
+        reg<OpLxor, x80>(MPIR_HIP_OP_LXOR, MPIR_HIP_F80);
+        reg_wide<OpSum, cx80>(MPIR_HIP_OP_SUM, MPIR_HIP_CF80);
+        reg_wide<OpProd, cx80>(MPIR_HIP_OP_PROD, MPIR_HIP_CF80);
+        reg_wide<OpMaxloc, pldint>(MPIR_HIP_OP_MAXLOC, MPIR_HIP_PLDOUBLEINT);
+        reg_wide<OpMinloc, pldint>(MPIR_HIP_OP_MINLOC, MPIR_HIP_PLDOUBLEINT);
         // REPLACE: a byte copy for every class (MPIR_Localcopy of a basic type)
         for (int e = 1; e < MPIR_HIP_NELEMS; ++e) reg<OpReplace, uint8_t>(MPIR_HIP_OP_REPLACE, e);
     }
@@ -99,8 +112,9 @@ struct MultiInit {
 } g_multi_init;
 
 const size_t g_elem_size[MPIR_HIP_NELEMS] = {
-    0, 1, 1, 2, 2, 4, 4, 8, 8, 2, 4, 8, 8, 16, 8, 8, 16, 8, 16,
+    0, 1, 1, 2, 2, 4, 4, 8, 8, 2, 4, 8, 8, 16, 8, 8, 16, 8, 16, 16, 32, 32,
 };
+static_assert(sizeof(g_elem_size) / sizeof(g_elem_size[0]) == MPIR_HIP_NELEMS, "one size per element class");
 
 // ------------------------------------------------------------ per-thread state
 constexpr int kMaxDev = 64;

@@ -171,6 +171,124 @@ hipError_t launch_reduce(const void *in_, void *io_, uint64_t count, hipStream_t
     return hipGetLastError();
 }
 
+// Elements wider than 16 bytes (long double _Complex, MPI_LONG_DOUBLE_INT:
+// 32 B).  Two variants:
+//   k_reduce_tile_wide     each lane loads its own elements' two 16-byte
+//                          halves (lanes 32 B apart: every wave instruction
+//                          touches each 128-byte line twice);
+//   k_reduce_tile_wide_lds the LDS transpose: the tile is loaded and stored
+//                          lane-contiguous (fully coalesced, `nt`), staged
+//                          through LDS, and each lane combines whole elements
+//                          out of LDS.
+// The buffer range check handles the ragged last tile (zeros in, stores dropped).
+template <class Op, class T, int EPL, int LPOL = kCachePolicyNT>
+__global__ __launch_bounds__(kThreads) void k_reduce_tile_wide(const char *in, char *io, uint64_t nbytes) {
+    static_assert(sizeof(T) == 32, "two 16-byte halves per element");
+    constexpr uint32_t tile = kThreads * EPL * 32;
+    const uint64_t base = (uint64_t)blockIdx.x * tile;
+    if (base >= nbytes) return;
+    const uint64_t left = nbytes - base;
+    const int nrec = (int)(left < tile ? left : tile);
+    __amdgpu_buffer_rsrc_t rin = __builtin_amdgcn_make_buffer_rsrc((void *)(in + base), 0, nrec, 0x00020000);
+    __amdgpu_buffer_rsrc_t rio = __builtin_amdgcn_make_buffer_rsrc((void *)(io + base), 0, nrec, 0x00020000);
+    u32x4 a[EPL][2], b[EPL][2];
+#pragma unroll
+    for (int u = 0; u < EPL; ++u) {
+        const int off = (u * kThreads + (int)threadIdx.x) * 32;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            a[u][h] = __builtin_amdgcn_raw_buffer_load_b128(rio, off + 16 * h, 0, LPOL);
+            b[u][h] = __builtin_amdgcn_raw_buffer_load_b128(rin, off + 16 * h, 0, LPOL);
+        }
+    }
+    Op op;
+    struct V { u32x4 h[2]; };
+#pragma unroll
+    for (int u = 0; u < EPL; ++u) {
+        const T x = __builtin_bit_cast(T, V{{a[u][0], a[u][1]}});
+        const T y = __builtin_bit_cast(T, V{{b[u][0], b[u][1]}});
+        const V r = __builtin_bit_cast(V, op(x, y));
+        const int off = (u * kThreads + (int)threadIdx.x) * 32;
+        __builtin_amdgcn_raw_buffer_store_b128(r.h[0], rio, off, 0, kCachePolicyNT);
+        __builtin_amdgcn_raw_buffer_store_b128(r.h[1], rio, off + 16, 0, kCachePolicyNT);
+    }
+}
+
+template <class Op, class T, int EPL>
+__global__ __launch_bounds__(kThreads) void k_reduce_tile_wide_lds(const char *in, char *io, uint64_t nbytes) {
+    static_assert(sizeof(T) == 32, "two 16-byte halves per element");
+    constexpr int NV = 2 * EPL;                       // 16-byte vectors per lane per operand
+    constexpr uint32_t tile = kThreads * NV * 16;
+    __shared__ u32x4 sa[kThreads * NV], sb[kThreads * NV];
+    const uint64_t base = (uint64_t)blockIdx.x * tile;
+    if (base >= nbytes) return;
+    const uint64_t left = nbytes - base;
+    const int nrec = (int)(left < tile ? left : tile);
+    __amdgpu_buffer_rsrc_t rin = __builtin_amdgcn_make_buffer_rsrc((void *)(in + base), 0, nrec, 0x00020000);
+    __amdgpu_buffer_rsrc_t rio = __builtin_amdgcn_make_buffer_rsrc((void *)(io + base), 0, nrec, 0x00020000);
+    const int t = (int)threadIdx.x;
+    u32x4 a[NV], b[NV];
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+        a[v] = __builtin_amdgcn_raw_buffer_load_b128(rio, (v * kThreads + t) * 16, 0, kCachePolicyNT);
+        b[v] = __builtin_amdgcn_raw_buffer_load_b128(rin, (v * kThreads + t) * 16, 0, kCachePolicyNT);
+    }
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+        sa[v * kThreads + t] = a[v];
+        sb[v * kThreads + t] = b[v];
+    }
+    __syncthreads();
+    Op op;
+    struct V { u32x4 h[2]; };
+#pragma unroll
+    for (int u = 0; u < EPL; ++u) {
+        const int e = u * kThreads + t;
+        const T x = __builtin_bit_cast(T, V{{sa[2 * e], sa[2 * e + 1]}});
+        const T y = __builtin_bit_cast(T, V{{sb[2 * e], sb[2 * e + 1]}});
+        const V r = __builtin_bit_cast(V, op(x, y));
+        sa[2 * e] = r.h[0];
+        sa[2 * e + 1] = r.h[1];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int v = 0; v < NV; ++v)
+        __builtin_amdgcn_raw_buffer_store_b128(sa[v * kThreads + t], rio, (v * kThreads + t) * 16, 0, kCachePolicyNT);
+}
+
+template <class Op, class T, int EPL, bool LDS>
+hipError_t launch_reduce_wide_x(const void *in_, void *io_, uint64_t count, hipStream_t s) {
+    const char *in = static_cast<const char *>(in_);
+    char *io = static_cast<char *>(io_);
+    constexpr uint32_t tile = kThreads * EPL * 32;
+    const uint64_t nbytes = count * sizeof(T);
+    uint64_t grid = (nbytes + tile - 1) / tile;
+    if (grid == 0) grid = 1;
+    if (LDS) hipLaunchKernelGGL((k_reduce_tile_wide_lds<Op, T, EPL>), dim3((unsigned)grid), dim3(kThreads), 0, s, in, io, nbytes);
+    else hipLaunchKernelGGL((k_reduce_tile_wide<Op, T, EPL, 0>), dim3((unsigned)grid), dim3(kThreads), 0, s, in, io, nbytes);
+    return hipGetLastError();
+}
+
+template <class Op, class T, int EPL = 2, int LPOL = kCachePolicyNT>
+hipError_t launch_reduce_wide(const void *in_, void *io_, uint64_t count, hipStream_t s) {
+    static_assert(sizeof(T) > 16, "16-byte and smaller elements use launch_reduce");
+    const char *in = static_cast<const char *>(in_);
+    char *io = static_cast<char *>(io_);
+    const uintptr_t ai = reinterpret_cast<uintptr_t>(in), ao = reinterpret_cast<uintptr_t>(io);
+    if (ai % 16 == 0 && ao % 16 == 0) {
+        constexpr uint32_t tile = kThreads * EPL * 32;
+        const uint64_t nbytes = count * sizeof(T);
+        uint64_t grid = (nbytes + tile - 1) / tile;
+        if (grid == 0) grid = 1;
+        hipLaunchKernelGGL((k_reduce_tile_wide<Op, T, EPL, LPOL>), dim3((unsigned)grid), dim3(kThreads), 0, s, in, io, nbytes);
+        return hipGetLastError();
+    }
+    uint64_t grid = (count + kThreads - 1) / kThreads;
+    if (grid > 4096) grid = 4096;
+    if (grid == 0) grid = 1;
+    hipLaunchKernelGGL((k_reduce_elems<Op, T, false>), dim3((unsigned)grid), dim3(kThreads), 0, s, in, io, count);
+    return hipGetLastError();
+}
 
 // ============================================================================
 // Multi-operand combines: the log2(p) / (p-1) MPIR_Reduce_local steps of a

@@ -19,9 +19,13 @@
 //     (oplxor.c:26 `((a)&&(!b))||((!a)&&(b))`).
 //   * MAXLOC/MINLOC: opmaxloc.c:48-59 / opminloc.c:48-59 -- take the winning
 //     pair; on equality loc = MPL_MIN(loc_a, loc_b); padding bytes untouched.
+//   * long double (MPI_LONG_DOUBLE, MPI_C_LONG_DOUBLE_COMPLEX,
+//     MPI_LONG_DOUBLE_INT): the x87 80-bit format in software (x87.hpp); every
+//     result is a 10-byte store, so the slot's 6 padding bytes keep inout's.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include "x87.hpp"
 
 namespace mpir_hip {
 
@@ -36,6 +40,16 @@ struct pfloatint { float value; int32_t loc; };                      //  8 B
 struct plongint  { int64_t value; int32_t loc; int32_t pad_; };      // 16 B
 struct pshortint { int16_t value; int16_t pad_; int32_t loc; };      //  8 B
 struct pdoubleint{ double value; int32_t loc; int32_t pad_; };       // 16 B
+struct pldint    { x80 value; int32_t loc; int32_t pad_[3]; };       // 32 B (MPI_LONG_DOUBLE_INT)
+struct cx80      { x80 re, im; };                                     // 32 B (long double _Complex)
+
+// b's value stored into a's slot: fstpt writes 10 bytes, a's padding stays
+__device__ __forceinline__ x80 x80_into(const x80 &b, const x80 &a) {
+    x80 r = a;
+    r.m = b.m;
+    r.se = b.se;
+    return r;
+}
 
 template <class T> struct uns { typedef T type; };
 template <> struct uns<int8_t>  { typedef uint8_t  type; };
@@ -94,6 +108,10 @@ struct OpSum {
     __device__ __forceinline__ double operator()(double a, double b) const { return xadd(a, b); }
     __device__ __forceinline__ cf32 operator()(cf32 a, cf32 b) const { return cf32{xadd(a.re, b.re), xadd(a.im, b.im)}; }
     __device__ __forceinline__ cf64 operator()(cf64 a, cf64 b) const { return cf64{xadd(a.re, b.re), xadd(a.im, b.im)}; }
+    __device__ __forceinline__ x80 operator()(x80 a, x80 b) const { return x80_add(a, b, a); }
+    __device__ __forceinline__ cx80 operator()(cx80 a, cx80 b) const {
+        return cx80{x80_add(a.re, b.re, a.re), x80_add(a.im, b.im, a.im)};
+    }
     // fast path for real types: a NaN operand or an invalid operation always
     // yields a NaN result, so the x86 rule only needs to run when the plain
     // result is NaN (see combine16 / fold_elems)
@@ -155,6 +173,10 @@ struct OpProd {
     __device__ __forceinline__ cf64 operator()(cf64 a, cf64 b) const {
         cf64 r; annexg_mul<double>(a.re, a.im, b.re, b.im, r.re, r.im); return r;
     }
+    __device__ __forceinline__ x80 operator()(x80 a, x80 b) const { return x80_mul(a, b, a); }
+    __device__ __forceinline__ cx80 operator()(cx80 a, cx80 b) const {
+        cx80 r; x80_cmul(a.re, a.im, b.re, b.im, r.re, r.im); return r;
+    }
     static constexpr bool kNanFast = true;
     template <class R> static __device__ __forceinline__ R raw(R a, R b) { return a * b; }
 };
@@ -175,9 +197,11 @@ template <class Op, class T> struct nan_fast {
 // MPL_MAX(a,b) (((a) > (b)) ? (a) : (b)); a = inout, b = in
 struct OpMax {
     template <class T> __device__ __forceinline__ T operator()(T a, T b) const { return (a > b) ? a : b; }
+    __device__ __forceinline__ x80 operator()(x80 a, x80 b) const { return x80_gt(a, b) ? a : x80_into(b, a); }
 };
 struct OpMin {
     template <class T> __device__ __forceinline__ T operator()(T a, T b) const { return (a < b) ? a : b; }
+    __device__ __forceinline__ x80 operator()(x80 a, x80 b) const { return x80_lt(a, b) ? a : x80_into(b, a); }
 };
 
 // ---------------------------------------------------------------- logical
@@ -192,6 +216,10 @@ struct OpLor {
 struct OpLxor {
     template <class T> __device__ __forceinline__ T operator()(T a, T b) const {
         return (T)((truth(a) && !truth(b)) || (!truth(a) && truth(b)));
+    }
+    // the 0/1 int result is converted (fildl) and stored with fstpt
+    __device__ __forceinline__ x80 operator()(x80 a, x80 b) const {
+        return (x80_truth(a) != x80_truth(b)) ? x80_one(a) : x80_zero(a);
     }
 };
 
@@ -209,12 +237,22 @@ struct OpMaxloc {
         else if (a.value <= b.value) a.loc = (a.loc < b.loc) ? a.loc : b.loc;
         return a;
     }
+    __device__ __forceinline__ pldint operator()(pldint a, pldint b) const {
+        if (x80_lt(a.value, b.value)) { a.value = x80_into(b.value, a.value); a.loc = b.loc; }
+        else if (x80_le(a.value, b.value)) a.loc = (a.loc < b.loc) ? a.loc : b.loc;
+        return a;
+    }
 };
 // opminloc.c:48-59 (mirror with > / >=)
 struct OpMinloc {
     template <class P> __device__ __forceinline__ P operator()(P a, P b) const {
         if (a.value > b.value) { a.value = b.value; a.loc = b.loc; }
         else if (a.value >= b.value) a.loc = (a.loc < b.loc) ? a.loc : b.loc;
+        return a;
+    }
+    __device__ __forceinline__ pldint operator()(pldint a, pldint b) const {
+        if (x80_gt(a.value, b.value)) { a.value = x80_into(b.value, a.value); a.loc = b.loc; }
+        else if (x80_ge(a.value, b.value)) a.loc = (a.loc < b.loc) ? a.loc : b.loc;
         return a;
     }
 };

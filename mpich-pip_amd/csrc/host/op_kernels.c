@@ -48,12 +48,14 @@ static const MPIR_Type_desc type_table[] = {
     /* FLOATING_POINT (:306-311) and _EXTRA (:315-319) */
     {MPI_FLOAT, MPIR_HIP_F32, G_FLOATING_POINT, "MPI_FLOAT"},
     {MPI_DOUBLE, MPIR_HIP_F64, G_FLOATING_POINT, "MPI_DOUBLE"},
+    {MPI_LONG_DOUBLE, MPIR_HIP_F80, G_FLOATING_POINT, "MPI_LONG_DOUBLE"},
     {MPIX_C_FLOAT16, MPIR_HIP_F16, G_FLOATING_EXTRA, "MPIX_C_FLOAT16"},
     /* LOGICAL (:324-327) */
     {MPI_C_BOOL, MPIR_HIP_U8, G_LOGICAL, "MPI_C_BOOL"},
     /* COMPLEX (:331-335) */
     {MPI_C_FLOAT_COMPLEX, MPIR_HIP_CF32, G_COMPLEX, "MPI_C_FLOAT_COMPLEX"},
     {MPI_C_DOUBLE_COMPLEX, MPIR_HIP_CF64, G_COMPLEX, "MPI_C_DOUBLE_COMPLEX"},
+    {MPI_C_LONG_DOUBLE_COMPLEX, MPIR_HIP_CF80, G_COMPLEX, "MPI_C_LONG_DOUBLE_COMPLEX"},
     /* BYTE (:344-345) */
     {MPI_BYTE, MPIR_HIP_U8, G_BYTE, "MPI_BYTE"},
     /* MAXLOC/MINLOC pairs (opmaxloc.c:83-97) */
@@ -62,6 +64,7 @@ static const MPIR_Type_desc type_table[] = {
     {MPI_LONG_INT, MPIR_HIP_PLONGINT, G_LOC_PAIR, "MPI_LONG_INT"},
     {MPI_SHORT_INT, MPIR_HIP_PSHORTINT, G_LOC_PAIR, "MPI_SHORT_INT"},
     {MPI_DOUBLE_INT, MPIR_HIP_PDOUBLEINT, G_LOC_PAIR, "MPI_DOUBLE_INT"},
+    {MPI_LONG_DOUBLE_INT, MPIR_HIP_PLDOUBLEINT, G_LOC_PAIR, "MPI_LONG_DOUBLE_INT"},
 };
 
 const MPIR_Type_desc *MPIR_Type_lookup(MPI_Datatype datatype)

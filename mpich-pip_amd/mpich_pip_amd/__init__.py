@@ -66,6 +66,7 @@ DATATYPES = {
     "MPI_LONG_LONG": 0x4C000809,
     "MPI_FLOAT": 0x4C00040A,
     "MPI_DOUBLE": 0x4C00080B,
+    "MPI_LONG_DOUBLE": 0x4C00100C,
     "MPI_BYTE": 0x4C00010D,
     "MPI_WCHAR": 0x4C00040E,
     "MPI_2INT": 0x4C000816,
@@ -73,6 +74,7 @@ DATATYPES = {
     "MPI_UNSIGNED_LONG_LONG": 0x4C000819,
     "MPI_FLOAT_INT": 0x8C000000,
     "MPI_DOUBLE_INT": 0x8C000001,
+    "MPI_LONG_DOUBLE_INT": 0x8C000004,
     "MPI_LONG_INT": 0x8C000002,
     "MPI_SHORT_INT": 0x8C000003,
     "MPI_INT8_T": 0x4C000137,
@@ -86,6 +88,7 @@ DATATYPES = {
     "MPI_C_BOOL": 0x4C00013F,
     "MPI_C_FLOAT_COMPLEX": 0x4C000840,
     "MPI_C_DOUBLE_COMPLEX": 0x4C001041,
+    "MPI_C_LONG_DOUBLE_COMPLEX": 0x4C002042,
     "MPIX_C_FLOAT16": 0x4C000246,
     "MPI_AINT": 0x4C000843,
     "MPI_OFFSET": 0x4C000844,

@@ -25,7 +25,10 @@
  *   - type groups per op                      mpir_op_util.h:263-364, op*.c
  *
  * Build configuration mirrored: x86-64, --disable-fortran, --disable-cxx,
- * no long double (MPID_NO_LONG_DOUBLE).  MPIX_C_FLOAT16 exists only when the
+ * with long double (MPI_LONG_DOUBLE, MPI_C_LONG_DOUBLE_COMPLEX,
+ * MPI_LONG_DOUBLE_INT; configure.ac:3456-3460,3486-3491,3699-3702): those
+ * loops are the reference's own shape on `long double`, so gcc compiles them
+ * to x87 instructions exactly as it compiles op*.c.  MPIX_C_FLOAT16 exists only when the
  * C compiler has _Float16 (configure.ac:3703-3705); gcc 11 on x86 does not,
  * so the reference's fp16 path is the AMD clang build.  clang lowers each
  * _Float16 operation on x86-64 (no AVX512-FP16) as extend-to-float, float
@@ -64,7 +67,8 @@
 #define E_OP 9
 
 enum { K_NONE, K_I8, K_U8, K_I16, K_U16, K_I32, K_U32, K_I64, K_U64, K_F16, K_F32, K_F64,
-       K_CF32, K_CF64, K_BOOL, K_P2INT, K_PFLOATINT, K_PLONGINT, K_PSHORTINT, K_PDOUBLEINT };
+       K_CF32, K_CF64, K_BOOL, K_P2INT, K_PFLOATINT, K_PLONGINT, K_PSHORTINT, K_PDOUBLEINT,
+       K_F80, K_CF80, K_PLDINT };
 
 /* groups */
 #define CI 0x001   /* C_INTEGER */
@@ -114,6 +118,9 @@ static int type_info(int dt, int *grp)
     case 0x8c000002: *grp = PR; return K_PLONGINT;
     case 0x8c000003: *grp = PR; return K_PSHORTINT;
     case 0x8c000001: *grp = PR; return K_PDOUBLEINT;
+    case 0x4c00100c: *grp = FP; return K_F80;    /* MPI_LONG_DOUBLE */
+    case 0x4c002042: *grp = CO; return K_CF80;   /* MPI_C_LONG_DOUBLE_COMPLEX */
+    case 0x8c000004: *grp = PR; return K_PLDINT; /* MPI_LONG_DOUBLE_INT */
     default: *grp = 0; return K_NONE;
     }
 }
@@ -274,6 +281,8 @@ static int apply(int opidx, int kind, const void *in, void *io, int len)
         case K_F64: FLOOP(double, d_quiet, LSUM); return 0;
         case K_CF32: LOOP(float _Complex, LSUM); return 0;
         case K_CF64: LOOP(double _Complex, LSUM); return 0;
+        case K_F80: LOOP(long double, LSUM); return 0;
+        case K_CF80: LOOP(long double _Complex, LSUM); return 0;
         }
         break;
     case 4:    /* PROD */
@@ -291,6 +300,8 @@ static int apply(int opidx, int kind, const void *in, void *io, int len)
         case K_F64: FLOOP(double, d_quiet, LPROD); return 0;
         case K_CF32: LOOP(float _Complex, LPROD); return 0;
         case K_CF64: LOOP(double _Complex, LPROD); return 0;
+        case K_F80: LOOP(long double, LPROD); return 0;
+        case K_CF80: LOOP(long double _Complex, LPROD); return 0;
         }
         break;
     case 1:    /* MAX */
@@ -300,7 +311,8 @@ static int apply(int opidx, int kind, const void *in, void *io, int len)
         case K_I16: LOOP(int16_t, F); return 0; case K_U16: LOOP(uint16_t, F); return 0; \
         case K_I32: LOOP(int32_t, F); return 0; case K_U32: LOOP(uint32_t, F); return 0; \
         case K_I64: LOOP(int64_t, F); return 0; case K_U64: LOOP(uint64_t, F); return 0; \
-        case K_F32: LOOP(float, F); return 0; case K_F64: LOOP(double, F); return 0; }
+        case K_F32: LOOP(float, F); return 0; case K_F64: LOOP(double, F); return 0; \
+        case K_F80: LOOP(long double, F); return 0; }
         if (opidx == 1) {
             if (kind == K_F16) { HLOOP_SEL(>); return 0; }
             SEL(LMAX)
@@ -323,6 +335,7 @@ static int apply(int opidx, int kind, const void *in, void *io, int len)
             if (kind == K_F16) { HLOOP_LXOR(); return 0; }
             if (kind == K_F32) { LOOP(float, LLXOR); return 0; }
             if (kind == K_F64) { LOOP(double, LLXOR); return 0; }
+            if (kind == K_F80) { LOOP(long double, LLXOR); return 0; }
             LOG(LLXOR)
         }
         break;
@@ -345,6 +358,7 @@ static int apply(int opidx, int kind, const void *in, void *io, int len)
         case K_PLONGINT: LOC_LOOP(long, int, <, <=); return 0;
         case K_PSHORTINT: LOC_LOOP(short, int, <, <=); return 0;
         case K_PDOUBLEINT: LOC_LOOP(double, int, <, <=); return 0;
+        case K_PLDINT: LOC_LOOP(long double, int, <, <=); return 0;
         }
         break;
     case 11:   /* MINLOC: opminloc.c:48-59 */
@@ -354,6 +368,7 @@ static int apply(int opidx, int kind, const void *in, void *io, int len)
         case K_PLONGINT: LOC_LOOP(long, int, >, >=); return 0;
         case K_PSHORTINT: LOC_LOOP(short, int, >, >=); return 0;
         case K_PDOUBLEINT: LOC_LOOP(double, int, >, >=); return 0;
+        case K_PLDINT: LOC_LOOP(long double, int, >, >=); return 0;
         }
         break;
     }
@@ -363,7 +378,7 @@ static int apply(int opidx, int kind, const void *in, void *io, int len)
 /* element size in bytes of an oracle kind */
 static int kind_size(int k)
 {
-    static const int sz[] = { 0, 1, 1, 2, 2, 4, 4, 8, 8, 2, 4, 8, 8, 16, 1, 8, 8, 16, 8, 16 };
+    static const int sz[] = { 0, 1, 1, 2, 2, 4, 4, 8, 8, 2, 4, 8, 8, 16, 1, 8, 8, 16, 8, 16, 16, 32, 32 };
     return sz[k];
 }
 

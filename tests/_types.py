@@ -1,6 +1,7 @@
 """Datatype table and seeded input generators shared by the parity tests.
 
-Every MPI basic type of the build (x86-64, no Fortran / C++ / long double),
+Every MPI basic type of the build (x86-64, no Fortran / C++; long double is
+the x87 80-bit format in a 16-byte slot),
 its numpy element representation, and the ops whose compute switch handles
 it (src/mpi/coll/op/op*.c).  Inputs are seeded uniform values with fixed
 positions overwritten by edge values (NaN, +-0, +-inf, denormals, INT_MIN /
@@ -19,8 +20,12 @@ INT = {"MPI_INT": "i4", "MPI_LONG": "i8", "MPI_SHORT": "i2", "MPI_UNSIGNED_SHORT
        "MPI_INT32_T": "i4", "MPI_INT64_T": "i8", "MPI_UINT8_T": "u1", "MPI_UINT16_T": "u2",
        "MPI_UINT32_T": "u4", "MPI_UINT64_T": "u8", "MPI_CHAR": "i1", "MPI_AINT": "i8", "MPI_OFFSET": "i8",
        "MPI_COUNT": "i8"}
-REAL = {"MPI_FLOAT": "f4", "MPI_DOUBLE": "f8", "MPIX_C_FLOAT16": "f2"}
-CPLX = {"MPI_C_FLOAT_COMPLEX": "c8", "MPI_C_DOUBLE_COMPLEX": "c16"}
+REAL = {"MPI_FLOAT": "f4", "MPI_DOUBLE": "f8", "MPIX_C_FLOAT16": "f2", "MPI_LONG_DOUBLE": "x80"}
+CPLX = {"MPI_C_FLOAT_COMPLEX": "c8", "MPI_C_DOUBLE_COMPLEX": "c16", "MPI_C_LONG_DOUBLE_COMPLEX": "cx80"}
+# x87 extended: 8-byte significand (explicit integer bit), 2-byte sign/exponent,
+# 6 padding bytes that a long double store never writes
+X80 = np.dtype([("m", "<u8"), ("se", "<u2"), ("pad", "V6")])
+CX80 = np.dtype([("re", X80), ("im", X80)])
 OTHER = {"MPI_C_BOOL": "b1", "MPI_BYTE": "u1"}
 PAIRS = {
     "MPI_2INT": np.dtype([("value", "<i4"), ("loc", "<i4")]),
@@ -28,6 +33,7 @@ PAIRS = {
     "MPI_LONG_INT": np.dtype([("value", "<i8"), ("loc", "<i4"), ("pad", "<i4")]),
     "MPI_SHORT_INT": np.dtype([("value", "<i2"), ("pad", "<i2"), ("loc", "<i4")]),
     "MPI_DOUBLE_INT": np.dtype([("value", "<f8"), ("loc", "<i4"), ("pad", "<i4")]),
+    "MPI_LONG_DOUBLE_INT": np.dtype([("value", X80), ("loc", "<i4"), ("pad", "V12")]),
 }
 ALL_TYPES = list(INT) + list(REAL) + list(CPLX) + list(OTHER) + list(PAIRS)
 
@@ -61,6 +67,10 @@ def check_ok(op: str, t: str) -> bool:
 def np_dtype(t: str) -> np.dtype:
     if t in PAIRS:
         return PAIRS[t]
+    if t == "MPI_LONG_DOUBLE":
+        return X80
+    if t == "MPI_C_LONG_DOUBLE_COMPLEX":
+        return CX80
     code = {**INT, **REAL, **CPLX, **OTHER}[t]
     return np.dtype({"f2": "<u2", "b1": "u1"}.get(code, "<" + code if code[0] != "b" else code))
 
@@ -77,9 +87,86 @@ F64_SPECIALS = [0x7FF8000000000000, 0xFFF8000000000000, 0x7FF0000000000000, 0xFF
 F16_SPECIALS = [0x7E00, 0xFE00, 0x7C00, 0xFC00, 0x0000, 0x8000, 0x0001, 0x83FF, 0x7BFF, 0x3C00, 0x7D01]
 
 
+def gen_x80(n: int, rng: np.random.Generator, specials: bool = True, pool: int = 0) -> np.ndarray:
+    """n x87 extended values as raw encodings: mostly normals (exponents near
+    1.0, some short significands for exact / tie cases, some across the range),
+    plus -- with specials -- denormals, pseudo-denormals, zeros, infinities,
+    quiet and signalling NaNs, unnormals and pseudo-NaN / pseudo-infinities.
+    Padding bytes are random (they must come through untouched).
+    pool > 0: draw from `pool` distinct values (many equal pairs, for MAXLOC)."""
+    x = np.zeros(n, dtype=X80)
+    m = rng.integers(0, 2 ** 63, n, dtype=np.uint64) | np.uint64(1 << 63)
+    short = rng.random(n) < 0.3
+    m[short] &= np.uint64(0xFFFFFF0000000000)
+    e = (0x3FFF - 20 + rng.integers(0, 40, n)).astype(np.uint16)
+    wide = rng.random(n) < 0.1
+    e[wide] = rng.integers(1, 0x7FFF, int(wide.sum())).astype(np.uint16)
+    sign = (rng.integers(0, 2, n) << 15).astype(np.uint16)
+    if specials:
+        k = rng.integers(0, 100, n)
+        cls = [(k < 3, 0, None), ((k >= 3) & (k < 5), 0, "pseudo"), ((k >= 5) & (k < 7), 0, "zero"),
+               ((k >= 7) & (k < 9), 0x7FFF, "inf"), ((k >= 9) & (k < 11), 0x7FFF, "qnan"),
+               ((k >= 11) & (k < 13), 0x7FFF, "snan"), ((k >= 13) & (k < 14), None, "unnormal"),
+               ((k >= 14) & (k < 15), 0x7FFF, "pseudonan")]
+        for mask, ev, kind in cls:
+            c = int(mask.sum())
+            if not c:
+                continue
+            r = rng.integers(0, 2 ** 62, c, dtype=np.uint64)
+            if kind is None:                     # denormal
+                mm = r >> rng.integers(0, 62, c).astype(np.uint64)
+            elif kind == "pseudo":
+                mm = r | np.uint64(1 << 63)
+            elif kind == "zero":
+                mm = np.zeros(c, np.uint64)
+            elif kind == "inf":
+                mm = np.full(c, 1 << 63, np.uint64)
+            elif kind == "qnan":
+                mm = r | np.uint64(3 << 62)
+            elif kind == "snan":
+                mm = (r >> np.uint64(1)) | np.uint64(1 << 63) | np.uint64(1)
+            elif kind == "unnormal":
+                mm = r
+            else:
+                mm = r
+            m[mask] = mm
+            if ev is None:
+                e[mask] = rng.integers(1, 0x7FFF, c).astype(np.uint16)
+            else:
+                e[mask] = ev
+    x["m"] = m
+    x["se"] = sign | e
+    x["pad"] = rng.integers(0, 256, (n, 6), dtype=np.uint8).view("V6").reshape(n)
+    if pool:
+        pick = rng.integers(0, min(pool, n), n)
+        x["m"], x["se"] = x["m"][pick], x["se"][pick]
+    return x
+
+
+def x80_nanish(v: np.ndarray) -> np.ndarray:
+    """x87 operands a compare finds unordered: NaNs and invalid encodings."""
+    e = v["se"] & 0x7FFF
+    j = (v["m"] >> np.uint64(63)) == 1
+    nan = (e == 0x7FFF) & j & ((v["m"] << np.uint64(1)) != 0)
+    invalid = ((e == 0x7FFF) & ~j) | ((e > 0) & (e < 0x7FFF) & ~j)
+    return nan | invalid
+
+
 def gen(t: str, n: int, rng: np.random.Generator, op: str = "MPI_SUM", specials: bool = True) -> np.ndarray:
     """n elements of type t; raw bit patterns for floats so NaN payloads survive."""
     dt = np_dtype(t)
+    if t == "MPI_LONG_DOUBLE":
+        return gen_x80(n, rng, specials)
+    if t == "MPI_C_LONG_DOUBLE_COMPLEX":
+        x = np.zeros(n, dtype=CX80)
+        x["re"], x["im"] = gen_x80(n, rng, specials), gen_x80(n, rng, specials)
+        return x
+    if t == "MPI_LONG_DOUBLE_INT":
+        x = np.zeros(n, dtype=dt)
+        x["value"] = gen_x80(n, rng, specials, pool=7)
+        x["loc"] = rng.integers(-1000, 1000, n)
+        x["pad"] = rng.integers(0, 256, (n, 12), dtype=np.uint8).view("V12").reshape(n)
+        return x
     if t in PAIRS:
         x = np.zeros(n, dtype=dt)
         vdt = dt["value"]

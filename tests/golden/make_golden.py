@@ -14,7 +14,11 @@ source:
        reference default count 10 (allred.c:390) and a ragged count 257;
      * the 3-element tests of test/mpi/coll/opsum.c:50-120,240-262,
        opmax.c:40-170, opmin.c:40-170, opprod.c:50-120 (char, signed char,
-       unsigned char, long long).
+       unsigned char, long long) and their long double blocks
+       (opsum.c:203-232, opmax.c:113-144, opmin.c:113-144, opprod.c:257-287,
+       oplxor.c:196-232, opmaxloc.c:265-310, opminloc.c:222-262), plus
+       allred.c's long double _Complex set4 member (:333-345).
+     Long double values are x87 80-bit encodings in a 16-byte slot, padding 0.
    An Allreduce over p ranks equals the fold acc = in_0;
    acc = Reduce_local(in_r, acc) for r = 1..p-1 (every op here is
    commutative and the KAT values make every fold order exact), so each case
@@ -52,6 +56,40 @@ SET2 = SET1 + [("MPI_FLOAT", 0x4C00040A, "f4"), ("MPI_DOUBLE", 0x4C00080B, "f8")
 SET3 = [("MPI_BYTE", 0x4C00010D, "u1")]
 SET4 = [("MPI_C_FLOAT_COMPLEX", 0x4C000840, "c8"), ("MPI_C_DOUBLE_COMPLEX", 0x4C001041, "c16")]
 SET5 = [("MPI_C_BOOL", 0x4C00013F, "b1")]
+SET4_LD = [("MPI_C_LONG_DOUBLE_COMPLEX", 0x4C002042, "cx80")]
+
+# x87 extended encodings (little-endian significand with explicit integer bit,
+# sign + 15-bit exponent, 6 padding bytes)
+X80 = np.dtype([("m", "<u8"), ("se", "<u2"), ("pad", "V6")])
+CX80 = np.dtype([("re", X80), ("im", X80)])
+LDINT = np.dtype([("a", X80), ("b", "<i4"), ("pad", "V12")])
+
+
+def x80_of_int(v):
+    """(significand, sign/exponent) of an integer exactly representable in 64 bits of significand."""
+    v = int(v)
+    sgn = 0x8000 if v < 0 else 0
+    n = abs(v)
+    if n == 0:
+        return 0, sgn
+    k = n.bit_length() - 1
+    m = n << (63 - k) if k <= 63 else n >> (k - 63)
+    assert (m << max(0, k - 63)) == n or k <= 63, v
+    return m, sgn | (16383 + k)
+
+
+def x80_arr(vals):
+    out = np.zeros(len(vals), dtype=X80)
+    for i, v in enumerate(vals):
+        out["m"][i], out["se"][i] = x80_of_int(v)
+    return out
+
+
+def cx80_arr(vals):
+    out = np.zeros(len(vals), dtype=CX80)
+    out["re"] = x80_arr(vals)
+    out["im"] = x80_arr([0] * len(vals))
+    return out
 
 OPS = {"MPI_MAX": 0x58000001, "MPI_MIN": 0x58000002, "MPI_SUM": 0x58000003, "MPI_PROD": 0x58000004,
        "MPI_LAND": 0x58000005, "MPI_BAND": 0x58000006, "MPI_LOR": 0x58000007, "MPI_BOR": 0x58000008,
@@ -120,6 +158,12 @@ def allred_cases(p, count):
             [cast(idx, code) for _ in range(p)],
             cast([power_seq(i, p, code) for i in idx], code) if code[0] not in "fc"
             else np.array([power_seq(i, p, code) for i in idx], dtype=NP[code]))
+    for tname, h, code in SET4_LD:
+        # allred.c set4 long double _Complex (:333-345): sum_test1 / prod_test1
+        add(f"allred_sum1_{tname}_p{p}_n{count}", "MPI_SUM", tname, h,
+            [cx80_arr(idx) for _ in range(p)], cx80_arr([i * p for i in idx]))
+        add(f"allred_prod1_{tname}_p{p}_n{count}", "MPI_PROD", tname, h,
+            [cx80_arr(idx) for _ in range(p)], cx80_arr([i ** p for i in idx]))
     for tname, h, code in SET2:
         # max_test1 / min_test1 (allred.c:178-194): in = i + rank.  The closed
         # form assumes no wrap (true at the reference's count 10); skip 1-byte
@@ -196,6 +240,36 @@ def opfile_cases(p):
             cast([fact[maxsize - 1], 0, 0], code))
 
 
+def opfile_long_double_cases(p):
+    """The HAVE_LONG_DOUBLE blocks of the op*.c tests (3 elements)."""
+    h, hi = 0x4C00100C, 0x8C000004
+    maxsize = min(p, 5)
+    fact = [1, 1, 2, 6, 24, 120]
+    add(f"opsum_MPI_LONG_DOUBLE_p{p}", "MPI_SUM", "MPI_LONG_DOUBLE", h,       # opsum.c:203-232
+        [x80_arr([1, 0, int(r > 0)]) for r in range(p)], x80_arr([p, 0, p - 1]))
+    add(f"opmax_MPI_LONG_DOUBLE_p{p}", "MPI_MAX", "MPI_LONG_DOUBLE", h,       # opmax.c:113-144
+        [x80_arr([1, 0, r]) for r in range(p)], x80_arr([1, 0, p - 1]))
+    add(f"opmin_MPI_LONG_DOUBLE_p{p}", "MPI_MIN", "MPI_LONG_DOUBLE", h,       # opmin.c:113-144
+        [x80_arr([1, 0, r]) for r in range(p)], x80_arr([1, 0, 0]))
+    add(f"opprod_MPI_LONG_DOUBLE_p{p}", "MPI_PROD", "MPI_LONG_DOUBLE", h,     # opprod.c:257-287
+        [x80_arr([r if 0 < r < maxsize else 1, 0, int(r > 0)]) for r in range(p)],
+        x80_arr([fact[maxsize - 1], 0, 0]))
+    add(f"oplxor_MPI_LONG_DOUBLE_p{p}", "MPI_LXOR", "MPI_LONG_DOUBLE", h,     # oplxor.c:196-232
+        [x80_arr([1, 0, int(r > 0)]) for r in range(p)], x80_arr([p % 2, 0, (p - 1) % 2]))
+    for op, sol in (("MPI_MAXLOC", [(1, 0), (0, 0), (p - 1, p - 1)]),        # opmaxloc.c:265-310
+                    ("MPI_MINLOC", [(1, 0), (0, 0), (0, 0)])):                 # opminloc.c:222-262
+        ranks = []
+        for r in range(p):
+            x = np.zeros(3, dtype=LDINT)
+            x["a"] = x80_arr([1, 0, r])
+            x["b"] = r
+            ranks.append(x)
+        want = np.zeros(3, dtype=LDINT)
+        want["a"] = x80_arr([v for v, _ in sol])
+        want["b"] = [l for _, l in sol]
+        add(f"{op[4:].lower()}_MPI_LONG_DOUBLE_INT_p{p}", op, "MPI_LONG_DOUBLE_INT", hi, ranks, want)
+
+
 def f32(x):
     return struct.unpack("<I", struct.pack("<f", x))[0]
 
@@ -250,6 +324,7 @@ def main():
         for count in (10, 257):
             allred_cases(p, count)
         opfile_cases(p)
+        opfile_long_double_cases(p)
     arrays, manifest = {}, []
     for k, c in enumerate(cases):
         arrays[f"c{k}_ranks"] = c["ranks"]
@@ -262,7 +337,8 @@ def main():
     digest = hashlib.sha256(open(npz, "rb").read()).hexdigest()
     with open(os.path.join(HERE, "kat_reference.json"), "w") as f:
         json.dump({"generator": "tests/golden/make_golden.py", "sha256_npz": digest,
-                   "source": "test/mpi/coll/allred.c, opsum.c, opmax.c, opmin.c, opprod.c closed forms",
+                   "source": "test/mpi/coll/allred.c, opsum.c, opmax.c, opmin.c, opprod.c, oplxor.c, opmaxloc.c, "
+                             "opminloc.c closed forms",
                    "cases": manifest}, f, indent=0)
     with open(os.path.join(HERE, "probe_survey.json"), "w") as f:
         json.dump({"generator": "tests/golden/make_golden.py",

@@ -76,6 +76,7 @@ def test_check_dtype_matches_oracle(mpi, orc):
 def test_has_kernel_for_every_compute_pair(mpi):
     """Every (op, type) the reference computes has a gfx950 kernel."""
     lib = mpi.load()
+    nelems = next(e for e in range(1, 256) if lib.MPIR_Hip_elem_size(e) == 0)
     elem_of = {}
     for t in T.ALL_TYPES:
         for op in T.OPS:
@@ -83,11 +84,12 @@ def test_has_kernel_for_every_compute_pair(mpi):
                 opidx = mpi.OPS[op] & 0xF
                 # resolve through the same path the op kernels use: a kernel must exist
                 found = any(lib.MPIR_Hip_has_kernel(opidx, e) and lib.MPIR_Hip_elem_size(e) == T.elem_size(t)
-                            for e in range(1, 19))
+                            for e in range(1, nelems))
                 assert found, (op, t)
         elem_of[t] = T.elem_size(t)
-    for e in range(1, 19):
-        assert lib.MPIR_Hip_elem_size(e) in (1, 2, 4, 8, 16)
+    assert nelems == 22
+    for e in range(1, nelems):
+        assert lib.MPIR_Hip_elem_size(e) in (1, 2, 4, 8, 16, 32)
 
 
 @pytest.mark.parametrize("op,dt,count,same,expect", [

@@ -104,7 +104,7 @@ def test_oracle_matrix_self_consistency(orc):
         for t in T.ALL_TYPES:
             chk = orc.check_dtype(m.OPS[op], m.DATATYPES[t])
             assert (chk == 0) == T.check_ok(op, t), (op, t)
-            x = np.zeros(16 * 4, dtype=np.uint8)
-            y = np.zeros(16 * 4, dtype=np.uint8)
+            x = np.zeros(32 * 4, dtype=np.uint8)
+            y = np.zeros(32 * 4, dtype=np.uint8)
             rc = orc.reduce_local(x, y, 4, m.DATATYPES[t], m.OPS[op], check=False)
             assert (rc == 0) == T.compute_ok(op, t), (op, t, rc)

@@ -58,6 +58,14 @@ def same(got: np.ndarray, want: np.ndarray, t: str) -> bool:
         return True
     if t not in T.CPLX:
         return False
+    if t == "MPI_C_LONG_DOUBLE_COMPLEX":
+        g, w = got.view(T.CX80), want.view(T.CX80)
+        ok = True
+        for part in ("re", "im"):
+            gp, wp = g[part], w[part]
+            value_eq = (gp["m"] == wp["m"]) & (gp["se"] == wp["se"])
+            ok &= bool(((value_eq | (T.x80_nanish(gp) & T.x80_nanish(wp))) & (gp["pad"] == wp["pad"])).all())
+        return ok
     ft = np.float32 if t == "MPI_C_FLOAT_COMPLEX" else np.float64
     ut = np.uint32 if ft == np.float32 else np.uint64
     g = got.view(ft)

@@ -177,7 +177,64 @@ int main(int argc, char **argv) {
             if (r >= 0) v.ms.push_back(ms);
         }
     }
+    // long double (software x87, x87.hpp): valid encodings in [1, 2) with random
+    // 64-bit significands, so every element takes the full add / mul path
+    std::vector<Var> lds = {
+        {"SUM long double", 16, &launch_reduce<OpSum, x80>, {}},
+        {"PROD long double", 16, &launch_reduce<OpProd, x80>, {}},
+        {"MAX long double", 16, &launch_reduce<OpMax, x80>, {}},
+        {"SUM long double _Complex E1", 32, &launch_reduce_wide<OpSum, cx80, 1>, {}},
+
+        {"SUM ld _Complex E1 ld-default", 32, &launch_reduce_wide<OpSum, cx80, 1, 0>, {}},
+        {"SUM ld _Complex E2 ld-default", 32, &launch_reduce_wide<OpSum, cx80, 2, 0>, {}},
+        {"SUM ld _Complex LDS E1", 32, &launch_reduce_wide_x<OpSum, cx80, 1, true>, {}},
+        {"SUM ld _Complex LDS E2", 32, &launch_reduce_wide_x<OpSum, cx80, 2, true>, {}},
+        {"MAXLOC ldint LDS E1", 32, &launch_reduce_wide_x<OpMaxloc, pldint, 1, true>, {}},
+        {"MAXLOC ldint LDS E2", 32, &launch_reduce_wide_x<OpMaxloc, pldint, 2, true>, {}},
+        {"PROD ld _Complex LDS E1", 32, &launch_reduce_wide_x<OpProd, cx80, 1, true>, {}},
+        {"PROD ld _Complex LDS E2", 32, &launch_reduce_wide_x<OpProd, cx80, 2, true>, {}},
+        {"MAXLOC ldint E2 ld-default", 32, &launch_reduce_wide<OpMaxloc, pldint, 2, 0>, {}},
+        {"PROD ld _Complex E2 ld-default", 32, &launch_reduce_wide<OpProd, cx80, 2, 0>, {}},
+        {"PROD long double _Complex E1", 32, &launch_reduce_wide<OpProd, cx80, 1>, {}},
+        {"PROD long double _Complex E2", 32, &launch_reduce_wide<OpProd, cx80, 2>, {}},
+
+        {"MAXLOC long double_int E2", 32, &launch_reduce_wide<OpMaxloc, pldint, 2>, {}},
+
+    };
+    {
+        std::vector<uint64_t> h(bytes / 8);
+        uint64_t x = 88172645463325252ull;
+        for (size_t i = 0; i < h.size(); i += 2) {
+            x ^= x << 13; x ^= x >> 7; x ^= x << 17;
+            h[i] = x | (1ull << 63);
+            h[i + 1] = 0x3fff;
+        }
+        for (int s = 0; s < NS; ++s) {
+            CK(hipMemcpy(in[s], h.data(), bytes, hipMemcpyHostToDevice));
+            CK(hipMemcpy(io[s], h.data(), bytes, hipMemcpyHostToDevice));
+        }
+        for (int r = -2; r < rounds; ++r)
+            for (auto &v : lds) {
+                int s = slot++ % NS;
+                // fresh inout every time so PROD / SUM never leave [1, 2^k)
+                CK(hipMemcpyAsync(io[s], in[(s + 1) % NS], bytes, hipMemcpyDeviceToDevice, st));
+                CK(hipEventRecord(e0, st));
+                CK(v.fn(in[s], io[s], bytes / v.esz, st));
+                CK(hipEventRecord(e1, st));
+                CK(hipEventSynchronize(e1));
+                float ms;
+                CK(hipEventElapsedTime(&ms, e0, e1));
+                if (r >= 0) v.ms.push_back(ms);
+            }
+    }
     printf("%zu MiB per operand, %d interleaved rounds\n", mib, rounds);
+    for (auto &v : lds) {
+        std::sort(v.ms.begin(), v.ms.end());
+        double med = v.ms[v.ms.size() / 2];
+        double gbs = 3.0 * bytes / (med * 1e-3) / 1e9;
+        printf("%-28s median %8.2f us  -> %7.0f GB/s  frac %.3f  (%.2f G elem/s)\n", v.name.c_str(), med * 1e3, gbs,
+               gbs / 8000.0, bytes / v.esz / (med * 1e-3) / 1e9);
+    }
     for (auto &v : mvs) {
         std::sort(v.ms.begin(), v.ms.end());
         double med = v.ms[v.ms.size() / 2];
