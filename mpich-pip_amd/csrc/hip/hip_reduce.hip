@@ -24,8 +24,8 @@ Entry g_table[MPIR_HIP_NOPS][MPIR_HIP_NELEMS];
 
 template <class Op, class T>
 void reg(int op, int elem) { g_table[op][elem].fn = &launch_reduce<Op, T>; }
-template <class Op, class T>
-void reg_wide(int op, int elem) { g_table[op][elem].fn = &launch_reduce_wide<Op, T>; }
+template <class Op, class T, int EPL = 2>
+void reg_wide(int op, int elem) { g_table[op][elem].fn = &launch_reduce_wide<Op, T, EPL>; }
 
 // Integer element classes and their device types.
 #define FOR_INTS(X) \
@@ -73,7 +73,7 @@ struct TableInit {
         reg<OpMin, x80>(MPIR_HIP_OP_MIN, MPIR_HIP_F80);
         reg<OpLxor, x80>(MPIR_HIP_OP_LXOR, MPIR_HIP_F80);
         reg_wide<OpSum, cx80>(MPIR_HIP_OP_SUM, MPIR_HIP_CF80);
-        reg_wide<OpProd, cx80>(MPIR_HIP_OP_PROD, MPIR_HIP_CF80);
+        reg_wide<OpProd, cx80, 1>(MPIR_HIP_OP_PROD, MPIR_HIP_CF80);
         reg_wide<OpMaxloc, pldint>(MPIR_HIP_OP_MAXLOC, MPIR_HIP_PLDOUBLEINT);
         reg_wide<OpMinloc, pldint>(MPIR_HIP_OP_MINLOC, MPIR_HIP_PLDOUBLEINT);
         // REPLACE: a byte copy for every class (MPIR_Localcopy of a basic type)

@@ -172,50 +172,16 @@ hipError_t launch_reduce(const void *in_, void *io_, uint64_t count, hipStream_t
 }
 
 // Elements wider than 16 bytes (long double _Complex, MPI_LONG_DOUBLE_INT:
-// 32 B).  Two variants:
-//   k_reduce_tile_wide     each lane loads its own elements' two 16-byte
-//                          halves (lanes 32 B apart: every wave instruction
-//                          touches each 128-byte line twice);
-//   k_reduce_tile_wide_lds the LDS transpose: the tile is loaded and stored
-//                          lane-contiguous (fully coalesced, `nt`), staged
-//                          through LDS, and each lane combines whole elements
-//                          out of LDS.
-// The buffer range check handles the ragged last tile (zeros in, stores dropped).
-template <class Op, class T, int EPL, int LPOL = kCachePolicyNT>
-__global__ __launch_bounds__(kThreads) void k_reduce_tile_wide(const char *in, char *io, uint64_t nbytes) {
-    static_assert(sizeof(T) == 32, "two 16-byte halves per element");
-    constexpr uint32_t tile = kThreads * EPL * 32;
-    const uint64_t base = (uint64_t)blockIdx.x * tile;
-    if (base >= nbytes) return;
-    const uint64_t left = nbytes - base;
-    const int nrec = (int)(left < tile ? left : tile);
-    __amdgpu_buffer_rsrc_t rin = __builtin_amdgcn_make_buffer_rsrc((void *)(in + base), 0, nrec, 0x00020000);
-    __amdgpu_buffer_rsrc_t rio = __builtin_amdgcn_make_buffer_rsrc((void *)(io + base), 0, nrec, 0x00020000);
-    u32x4 a[EPL][2], b[EPL][2];
-#pragma unroll
-    for (int u = 0; u < EPL; ++u) {
-        const int off = (u * kThreads + (int)threadIdx.x) * 32;
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            a[u][h] = __builtin_amdgcn_raw_buffer_load_b128(rio, off + 16 * h, 0, LPOL);
-            b[u][h] = __builtin_amdgcn_raw_buffer_load_b128(rin, off + 16 * h, 0, LPOL);
-        }
-    }
-    Op op;
-    struct V { u32x4 h[2]; };
-#pragma unroll
-    for (int u = 0; u < EPL; ++u) {
-        const T x = __builtin_bit_cast(T, V{{a[u][0], a[u][1]}});
-        const T y = __builtin_bit_cast(T, V{{b[u][0], b[u][1]}});
-        const V r = __builtin_bit_cast(V, op(x, y));
-        const int off = (u * kThreads + (int)threadIdx.x) * 32;
-        __builtin_amdgcn_raw_buffer_store_b128(r.h[0], rio, off, 0, kCachePolicyNT);
-        __builtin_amdgcn_raw_buffer_store_b128(r.h[1], rio, off + 16, 0, kCachePolicyNT);
-    }
-}
-
+// 32 B): the LDS transpose.  The tile is loaded and stored lane-contiguous
+// (fully coalesced buffer_load/store_dwordx4 nt, like k_reduce_tile), staged
+// through LDS, and each lane combines whole elements out of LDS -- the soft
+// x87 combine needs an element's two 16-byte halves in one lane.  Measured at
+// 256 MiB (profiles/r01_kernel_ab_wide_lds.log): SUM 0.78, MAXLOC 0.81 of the
+// HBM peak vs 0.65 when each lane loads its own halves (lanes 32 B apart, every
+// 128-byte line fetched twice under `nt`).  The buffer range check handles
+// the ragged last tile (zeros in, stores dropped).
 template <class Op, class T, int EPL>
-__global__ __launch_bounds__(kThreads) void k_reduce_tile_wide_lds(const char *in, char *io, uint64_t nbytes) {
+__global__ __launch_bounds__(kThreads) void k_reduce_tile_wide(const char *in, char *io, uint64_t nbytes) {
     static_assert(sizeof(T) == 32, "two 16-byte halves per element");
     constexpr int NV = 2 * EPL;                       // 16-byte vectors per lane per operand
     constexpr uint32_t tile = kThreads * NV * 16;
@@ -256,20 +222,10 @@ __global__ __launch_bounds__(kThreads) void k_reduce_tile_wide_lds(const char *i
         __builtin_amdgcn_raw_buffer_store_b128(sa[v * kThreads + t], rio, (v * kThreads + t) * 16, 0, kCachePolicyNT);
 }
 
-template <class Op, class T, int EPL, bool LDS>
-hipError_t launch_reduce_wide_x(const void *in_, void *io_, uint64_t count, hipStream_t s) {
-    const char *in = static_cast<const char *>(in_);
-    char *io = static_cast<char *>(io_);
-    constexpr uint32_t tile = kThreads * EPL * 32;
-    const uint64_t nbytes = count * sizeof(T);
-    uint64_t grid = (nbytes + tile - 1) / tile;
-    if (grid == 0) grid = 1;
-    if (LDS) hipLaunchKernelGGL((k_reduce_tile_wide_lds<Op, T, EPL>), dim3((unsigned)grid), dim3(kThreads), 0, s, in, io, nbytes);
-    else hipLaunchKernelGGL((k_reduce_tile_wide<Op, T, EPL, 0>), dim3((unsigned)grid), dim3(kThreads), 0, s, in, io, nbytes);
-    return hipGetLastError();
-}
-
-template <class Op, class T, int EPL = 2, int LPOL = kCachePolicyNT>
+// EPL: elements per lane (2 for the memory-bound ops; the compute-bound soft
+// x87 complex PROD does better with 1, more waves per element).
+// Pointers not 16 B-aligned take the element-granular kernel.
+template <class Op, class T, int EPL = 2>
 hipError_t launch_reduce_wide(const void *in_, void *io_, uint64_t count, hipStream_t s) {
     static_assert(sizeof(T) > 16, "16-byte and smaller elements use launch_reduce");
     const char *in = static_cast<const char *>(in_);
@@ -280,7 +236,7 @@ hipError_t launch_reduce_wide(const void *in_, void *io_, uint64_t count, hipStr
         const uint64_t nbytes = count * sizeof(T);
         uint64_t grid = (nbytes + tile - 1) / tile;
         if (grid == 0) grid = 1;
-        hipLaunchKernelGGL((k_reduce_tile_wide<Op, T, EPL, LPOL>), dim3((unsigned)grid), dim3(kThreads), 0, s, in, io, nbytes);
+        hipLaunchKernelGGL((k_reduce_tile_wide<Op, T, EPL>), dim3((unsigned)grid), dim3(kThreads), 0, s, in, io, nbytes);
         return hipGetLastError();
     }
     uint64_t grid = (count + kThreads - 1) / kThreads;

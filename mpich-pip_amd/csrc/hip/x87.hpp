@@ -186,6 +186,25 @@ X87_FN x80 x80_mul(x80 a, x80 b, const x80 &pad) {
     }
     if (ca == X80_ZERO || cb == X80_ZERO) return x80_make(s, 0, 0, pad);
     const u128 prod = (u128)a.m * (u128)b.m;       // value = prod * 2^(Ea + Eb - 126)
+    if (ca == X80_NORMAL && cb == X80_NORMAL) {
+        // both significands in [2^63, 2^64): the product's leading one is at
+        // bit 126 or 127, so the rounding position is fixed (no 128-bit shifter)
+        const bool top = (uint64_t)(prod >> 127) != 0;
+        const int er = (int)(a.se & 0x7fff) + (int)(b.se & 0x7fff) - 16383 + (top ? 1 : 0);
+        if (er >= 1 && er <= 0x7ffe) {
+            const uint64_t hi = (uint64_t)(prod >> 64), lo = (uint64_t)prod;
+            uint64_t sig, rem, half;
+            if (top) { sig = hi; rem = lo; half = 1ull << 63; }
+            else { sig = (hi << 1) | (lo >> 63); rem = lo & ~(1ull << 63); half = 1ull << 62; }
+            if (rem > half || (rem == half && (sig & 1))) {
+                if (++sig == 0) {
+                    if (er + 1 >= 0x7fff) return x80_make(s, 0x7fff, 1ull << 63, pad);
+                    return x80_make(s, (uint32_t)(er + 1), 1ull << 63, pad);
+                }
+            }
+            return x80_make(s, (uint32_t)er, sig, pad);
+        }
+    }
     return x80_round_pack(s, x80_uexp(a) + x80_uexp(b) - 126, prod, pad);
 }
 

@@ -183,24 +183,12 @@ int main(int argc, char **argv) {
         {"SUM long double", 16, &launch_reduce<OpSum, x80>, {}},
         {"PROD long double", 16, &launch_reduce<OpProd, x80>, {}},
         {"MAX long double", 16, &launch_reduce<OpMax, x80>, {}},
-        {"SUM long double _Complex E1", 32, &launch_reduce_wide<OpSum, cx80, 1>, {}},
-
-        {"SUM ld _Complex E1 ld-default", 32, &launch_reduce_wide<OpSum, cx80, 1, 0>, {}},
-        {"SUM ld _Complex E2 ld-default", 32, &launch_reduce_wide<OpSum, cx80, 2, 0>, {}},
-        {"SUM ld _Complex LDS E1", 32, &launch_reduce_wide_x<OpSum, cx80, 1, true>, {}},
-        {"SUM ld _Complex LDS E2", 32, &launch_reduce_wide_x<OpSum, cx80, 2, true>, {}},
-        {"MAXLOC ldint LDS E1", 32, &launch_reduce_wide_x<OpMaxloc, pldint, 1, true>, {}},
-        {"MAXLOC ldint LDS E2", 32, &launch_reduce_wide_x<OpMaxloc, pldint, 2, true>, {}},
-        {"PROD ld _Complex LDS E1", 32, &launch_reduce_wide_x<OpProd, cx80, 1, true>, {}},
-        {"PROD ld _Complex LDS E2", 32, &launch_reduce_wide_x<OpProd, cx80, 2, true>, {}},
-        {"MAXLOC ldint E2 ld-default", 32, &launch_reduce_wide<OpMaxloc, pldint, 2, 0>, {}},
-        {"PROD ld _Complex E2 ld-default", 32, &launch_reduce_wide<OpProd, cx80, 2, 0>, {}},
-        {"PROD long double _Complex E1", 32, &launch_reduce_wide<OpProd, cx80, 1>, {}},
+        {"SUM long double _Complex (E2)", 32, &launch_reduce_wide<OpSum, cx80, 2>, {}},
+        {"PROD long double _Complex (E1)", 32, &launch_reduce_wide<OpProd, cx80, 1>, {}},
         {"PROD long double _Complex E2", 32, &launch_reduce_wide<OpProd, cx80, 2>, {}},
-
-        {"MAXLOC long double_int E2", 32, &launch_reduce_wide<OpMaxloc, pldint, 2>, {}},
-
+        {"MAXLOC long double_int (E2)", 32, &launch_reduce_wide<OpMaxloc, pldint, 2>, {}},
     };
+
     {
         std::vector<uint64_t> h(bytes / 8);
         uint64_t x = 88172645463325252ull;
