@@ -42,7 +42,7 @@ def run_ranks(fn, p, timeout=120):
 
 CASES = [("MPI_FLOAT", "MPI_SUM"), ("MPIX_C_FLOAT16", "MPI_SUM"), ("MPI_INT", "MPI_SUM"),
          ("MPI_DOUBLE", "MPI_MAX"), ("MPI_UNSIGNED_CHAR", "MPI_BXOR"), ("MPI_C_DOUBLE_COMPLEX", "MPI_SUM"),
-         ("MPI_DOUBLE_INT", "MPI_MAXLOC")]
+         ("MPI_DOUBLE_INT", "MPI_MAXLOC"), ("MPI_LONG_DOUBLE", "MPI_SUM"), ("MPI_C_LONG_DOUBLE_COMPLEX", "MPI_PROD")]
 
 
 @pytest.mark.parametrize("t,op", CASES, ids=[f"{t}-{o}" for t, o in CASES])
@@ -82,7 +82,8 @@ def test_allreduce_reference_order(mpi, orc, cuda, t, op, p, inplace):
 
 
 @pytest.mark.parametrize("t,op", [("MPIX_C_FLOAT16", "MPI_SUM"), ("MPI_FLOAT", "MPI_SUM"), ("MPI_INT64_T", "MPI_PROD"),
-                                  ("MPI_UNSIGNED", "MPI_BAND"), ("MPI_FLOAT", "MPI_MIN")])
+                                  ("MPI_UNSIGNED", "MPI_BAND"), ("MPI_FLOAT", "MPI_MIN"),
+                                  ("MPI_LONG_DOUBLE_INT", "MPI_MINLOC")])
 @pytest.mark.parametrize("p", [1, 2, 3, 8])
 @pytest.mark.parametrize("inplace", [False, True])
 def test_reduce_scatter_block_reference_order(mpi, orc, cuda, t, op, p, inplace):
