@@ -118,13 +118,43 @@ static_assert(sizeof(g_elem_size) / sizeof(g_elem_size[0]) == MPIR_HIP_NELEMS, "
 
 // ------------------------------------------------------------ per-thread state
 constexpr int kMaxDev = 64;
-constexpr uint64_t kStageChunk = 64ull << 20;  // bytes per operand per staging chunk
+constexpr int kMaxStageSlots = 8;
+
+// Staging of host (or other-device) operands: chunks of `stage_chunk()` bytes
+// per operand flow through a three-stage pipeline -- H2D copies on stream
+// "up", the kernel on "comp", the D2H copy-back on "down" -- over
+// `stage_slots()` device scratch slots, so host->device and device->host
+// transfers run at the same time (PCIe is full duplex).  Events order the
+// stages of one chunk and stop a slot from being refilled before its
+// copy-back has read it.
+// MPIR_CVAR_REDUCE_LOCAL_STAGE_CHUNK_MB / MPIR_CVAR_REDUCE_LOCAL_STAGE_SLOTS override.
+uint64_t stage_chunk() {
+    static uint64_t v = 0;
+    if (!v) {
+        const char *e = getenv("MPIR_CVAR_REDUCE_LOCAL_STAGE_CHUNK_MB");
+        const long mb = e ? atol(e) : 0;
+        v = (uint64_t)(mb > 0 && mb <= 1024 ? mb : 32) << 20;
+    }
+    return v;
+}
+int stage_slots() {
+    static int v = 0;
+    if (!v) {
+        const char *e = getenv("MPIR_CVAR_REDUCE_LOCAL_STAGE_SLOTS");
+        const int n = e ? atoi(e) : 0;
+        v = n >= 2 && n <= kMaxStageSlots ? n : 3;
+    }
+    return v;
+}
+
+enum { S_MAIN = 0, S_UP = 1, S_COMP = 2, S_DOWN = 3, S_NSTREAMS = 4 };
 
 struct DevCtx {
-    hipStream_t stream[2] = {nullptr, nullptr};
+    hipStream_t stream[S_NSTREAMS] = {nullptr, nullptr, nullptr, nullptr};
+    hipEvent_t ev_up[kMaxStageSlots] = {}, ev_comp[kMaxStageSlots] = {}, ev_free[kMaxStageSlots] = {};
     volatile uint32_t *flag = nullptr;   // pinned completion word (wait mode "flag")
     uint32_t seq = 0;
-    char *scratch = nullptr;     // 2 slots x (in, inout) x kStageChunk
+    char *scratch = nullptr;     // staging slots x (in, inout) x chunk, or multi-operand temporaries
     size_t scratch_bytes = 0;
 };
 
@@ -150,6 +180,16 @@ int get_stream(int dev, int slot, hipStream_t *out) {
         HIPCHK(hipStreamCreate(&d.stream[slot]));
     }
     *out = d.stream[slot];
+    return MPIR_HIP_OK;
+}
+
+int get_stage_events(int dev, int nslots) {
+    DevCtx &d = t_ctx.dev[dev];
+    for (int k = 0; k < nslots; ++k) {
+        if (!d.ev_up[k]) HIPCHK(hipEventCreateWithFlags(&d.ev_up[k], hipEventDisableTiming));
+        if (!d.ev_comp[k]) HIPCHK(hipEventCreateWithFlags(&d.ev_comp[k], hipEventDisableTiming));
+        if (!d.ev_free[k]) HIPCHK(hipEventCreateWithFlags(&d.ev_free[k], hipEventDisableTiming));
+    }
     return MPIR_HIP_OK;
 }
 
@@ -287,7 +327,7 @@ int MPIR_Hip_combine(const void *const *inbufs, int n, void *outbuf, uint64_t co
     if (cur != dev) HIPCHK(hipSetDevice(dev));
     hipStream_t s = (hipStream_t)hip_stream;
     int rc = MPIR_HIP_OK;
-    if (!s) rc = get_stream(dev, 0, &s);
+    if (!s) rc = get_stream(dev, S_MAIN, &s);
     hipError_t e = hipSuccess;
     if (rc == MPIR_HIP_OK && count > 0) {
         const bool fused = g_multi[op][elem][0][0] != nullptr;
@@ -304,8 +344,10 @@ int MPIR_Hip_combine(const void *const *inbufs, int n, void *outbuf, uint64_t co
                 // outbuf, v_j (j > 0 even) in device scratch.
                 const uint64_t bytes = count * esz, slot = (bytes + 255) & ~(uint64_t)255;
                 const uint64_t unit = (op == MPIR_HIP_OP_REPLACE) ? 1 : esz;
+                // stream-ordered temporaries (hipMallocAsync): safe when calls on
+                // different streams overlap
                 char *scr = nullptr;
-                if (n > 2) rc = get_scratch(dev, (size_t)(n / 2 - 1) * slot, &scr);
+                if (n > 2) e = hipMallocAsync((void **)&scr, (size_t)(n / 2 - 1) * slot, s);
                 void *v[64];
                 for (int j = 0; j < n && rc == MPIR_HIP_OK; ++j) v[j] = const_cast<void *>(inbufs[j]);
                 for (int step = 1; step < n && rc == MPIR_HIP_OK && e == hipSuccess; step *= 2) {
@@ -317,6 +359,10 @@ int MPIR_Hip_combine(const void *const *inbufs, int n, void *outbuf, uint64_t co
                         }
                         if (e == hipSuccess) e = g_table[op][elem].fn(v[j + step], v[j], bytes / unit, s);
                     }
+                }
+                if (scr) {
+                    const hipError_t ef = hipFreeAsync(scr, s);
+                    if (e == hipSuccess) e = ef;
                 }
             }
         } else {
@@ -371,7 +417,7 @@ int MPIR_Hip_reduce(const void *inbuf, void *inoutbuf, uint64_t count, int op, i
         if (cur != dio) HIPCHK(hipSetDevice(dio));
         hipStream_t s = (hipStream_t)hip_stream;
         int rc = MPIR_HIP_OK;
-        if (!s) rc = get_stream(dio, 0, &s);
+        if (!s) rc = get_stream(dio, S_MAIN, &s);
         if (rc == MPIR_HIP_OK) {
             hipError_t e = fn(inbuf, inoutbuf, count * esz / unit, s);
             if (e != hipSuccess) rc = set_err(e, "kernel launch");
@@ -383,8 +429,8 @@ int MPIR_Hip_reduce(const void *inbuf, void *inoutbuf, uint64_t count, int op, i
     if (!sync) return MPIR_HIP_EBUFFER;  // the stream variant needs device buffers
 
     // ---- staged path: at least one operand is host memory (or the two ----
-    // ---- operands live on different devices).  Chunks ping-pong over  ----
-    // ---- two streams so the copies of chunk k+1 overlap chunk k.      ----
+    // ---- operands live on different devices): the up / comp / down      ----
+    // ---- pipeline described at stage_chunk().                            ----
     int dev = 0;
     if (lio == LOC_DEVICE) dev = dio;
     else if (lin == LOC_DEVICE) dev = din;
@@ -397,37 +443,51 @@ int MPIR_Hip_reduce(const void *inbuf, void *inoutbuf, uint64_t count, int op, i
     if (cur != dev) HIPCHK(hipSetDevice(dev));
 
     int rc = MPIR_HIP_OK;
+    DevCtx &d = t_ctx.dev[dev];
     const bool stage_in = !(lin == LOC_DEVICE && din == dev);
     const bool stage_io = !(lio == LOC_DEVICE && dio == dev);
     const uint64_t total = count * esz;
-    uint64_t chunk_elems = kStageChunk / esz;
+    uint64_t chunk_elems = stage_chunk() / esz;
     if (chunk_elems > count) chunk_elems = count;
     const uint64_t chunk_bytes = chunk_elems * esz;
-    char *scratch = nullptr;
-    hipStream_t st[2];
-    rc = get_scratch(dev, 4 * ((chunk_bytes + 255) & ~(uint64_t)255), &scratch);
-    if (rc == MPIR_HIP_OK) rc = get_stream(dev, 0, &st[0]);
-    if (rc == MPIR_HIP_OK) rc = get_stream(dev, 1, &st[1]);
     const uint64_t slot_bytes = (chunk_bytes + 255) & ~(uint64_t)255;
+    const int nslots = stage_slots();
+    char *scratch = nullptr;
+    hipStream_t up = nullptr, comp = nullptr, down = nullptr;
+    rc = get_scratch(dev, (size_t)(2 * nslots) * slot_bytes, &scratch);
+    if (rc == MPIR_HIP_OK) rc = get_stream(dev, S_UP, &up);
+    if (rc == MPIR_HIP_OK) rc = get_stream(dev, S_COMP, &comp);
+    if (rc == MPIR_HIP_OK) rc = get_stream(dev, S_DOWN, &down);
+    if (rc == MPIR_HIP_OK) rc = get_stage_events(dev, nslots);
     const char *cin = static_cast<const char *>(inbuf);
     char *cio = static_cast<char *>(inoutbuf);
     for (uint64_t off = 0, k = 0; rc == MPIR_HIP_OK && off < total; off += chunk_bytes, ++k) {
         const uint64_t nb = (total - off < chunk_bytes) ? total - off : chunk_bytes;
-        const int slot = (int)(k & 1);
-        hipStream_t s = st[slot];
+        const int slot = (int)(k % (uint64_t)nslots);
         char *sin = scratch + (2 * slot) * slot_bytes;
         char *sio = scratch + (2 * slot + 1) * slot_bytes;
-        const void *kin = cin + off;
-        void *kio = cio + off;
+        const void *kin = stage_in ? (const void *)sin : (const void *)(cin + off);
+        void *kio = stage_io ? (void *)sio : (void *)(cio + off);
         hipError_t e = hipSuccess;
-        if (stage_in) { e = hipMemcpyAsync(sin, cin + off, nb, hipMemcpyDefault, s); kin = sin; }
-        if (e == hipSuccess && stage_io) { e = hipMemcpyAsync(sio, cio + off, nb, hipMemcpyDefault, s); kio = sio; }
-        if (e == hipSuccess) e = fn(kin, kio, nb / unit, s);
-        if (e == hipSuccess && stage_io) e = hipMemcpyAsync(cio + off, sio, nb, hipMemcpyDefault, s);
+        // the slot's previous chunk must be fully consumed (kernel read, copy-back done)
+        if (k >= (uint64_t)nslots) e = hipStreamWaitEvent(up, d.ev_free[slot], 0);
+        if (e == hipSuccess && stage_in) e = hipMemcpyAsync(sin, cin + off, nb, hipMemcpyDefault, up);
+        if (e == hipSuccess && stage_io) e = hipMemcpyAsync(sio, cio + off, nb, hipMemcpyDefault, up);
+        if (e == hipSuccess) e = hipEventRecord(d.ev_up[slot], up);
+        if (e == hipSuccess) e = hipStreamWaitEvent(comp, d.ev_up[slot], 0);
+        if (e == hipSuccess) e = fn(kin, kio, nb / unit, comp);
+        if (e == hipSuccess) e = hipEventRecord(d.ev_comp[slot], comp);
+        if (stage_io) {
+            if (e == hipSuccess) e = hipStreamWaitEvent(down, d.ev_comp[slot], 0);
+            if (e == hipSuccess) e = hipMemcpyAsync(cio + off, sio, nb, hipMemcpyDefault, down);
+            if (e == hipSuccess) e = hipEventRecord(d.ev_free[slot], down);
+        } else if (e == hipSuccess) {
+            e = hipEventRecord(d.ev_free[slot], comp);
+        }
         if (e != hipSuccess) rc = set_err(e, "staged reduce");
     }
-    if (rc == MPIR_HIP_OK) rc = wait_stream_block(st[0]);
-    if (rc == MPIR_HIP_OK) rc = wait_stream_block(st[1]);
+    if (rc == MPIR_HIP_OK) rc = wait_stream_block(comp);
+    if (rc == MPIR_HIP_OK) rc = wait_stream_block(down);
     if (cur != dev) (void)hipSetDevice(cur);
     return rc;
 }
