@@ -70,7 +70,8 @@ int MPIR_Hip_reduce(const void *inbuf, void *inoutbuf, uint64_t count, int op, i
 /* Multi-operand combine: outbuf = fold(inbufs[0..n-1]) in one pass, in the
  * association of a reduction schedule (the schedule's MPIR_Reduce_local steps
  * fused; left operand = the step's inoutbuf):
- *   MPIR_HIP_ORDER_TREE  (n = 1, 2, 4, 8): ((y0+y1)+(y2+y3))+((y4+y5)+(y6+y7)),
+ *   MPIR_HIP_ORDER_TREE  (n a power of two <= 64; one fused pass for n <= 8):
+ *       ((y0+y1)+(y2+y3))+((y4+y5)+(y6+y7)),
  *       the recursive-halving order of reduce_intra_reduce_scatter_gather.c;
  *   MPIR_HIP_ORDER_CHAIN (1 <= n <= 64): ((y0+y1)+y2)+..., the pairwise order
  *       of reduce_scatter_block_intra_pairwise.c.

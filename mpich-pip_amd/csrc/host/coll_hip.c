@@ -31,6 +31,8 @@
 #define COMM_RCCL 1
 #define COMM_LOOPBACK 2
 #define MAX_XFER 256
+#define REDUCE_SHORT_MSG_SIZE 2048            /* reduce.c:14-17 */
+#define RSB_COMMUTATIVE_LONG_MSG_SIZE 524288  /* reduce_scatter.c:14-17 */
 
 typedef struct {
     void *buf;
@@ -366,6 +368,139 @@ static void cnts_disps(long count, int pof2, long *cnts, long *disps)
         disps[i] = disps[i - 1] + cnts[i - 1];
 }
 
+/* ------------------------------------------------------------ short messages
+ * MPICH switches algorithm on message size.  For these the device form keeps
+ * the reference's association and operand order but not its rounds: ONE
+ * exchange brings a rank every operand it needs, then the schedule's fold runs
+ * on the device (tests/test_schedule_small_cpu.py pins the fold plans against
+ * step-by-step simulations of the reference). */
+static int hip_err(const char *fc, hipError_t e)
+{
+    MPIR_Err_set_detail("%s: HIP error %s", fc, hipGetErrorString(e));
+    return MPI_ERR_OTHER;
+}
+
+static int fold_tree(const void *const *ys, int n, void *out, long count, int opidx, int elem, hipStream_t s,
+                     const char *fc)
+{
+    int rc = MPIR_Hip_combine(ys, n, out, (uint64_t) count, opidx, elem, MPIR_HIP_ORDER_TREE, s, 0);
+    if (rc) {
+        MPIR_Op_report_hip_error(fc, rc);
+        return MPI_ERR_OTHER;
+    }
+    return MPI_SUCCESS;
+}
+
+static int fold_step(const void *src, void *dst, long count, int opidx, int elem, hipStream_t s, const char *fc)
+{
+    int rc = MPIR_Hip_reduce(src, dst, (uint64_t) count, opidx, elem, s, 0);
+    if (rc) {
+        MPIR_Op_report_hip_error(fc, rc);
+        return MPI_ERR_OTHER;
+    }
+    return MPI_SUCCESS;
+}
+
+/* MPI_Allreduce, count*size <= 2048 or count < pof2: MPIR_Reduce takes the
+ * binomial tree to root 0 (reduce.c:214-225, reduce_intra_binomial.c:93-140:
+ * relrank r folds in the accumulation of r|mask as the second operand), then
+ * MPIR_Bcast.  Here: an allgather of the p inputs into slots 0..p-1, then every
+ * rank folds them in the binomial order itself, so all ranks hold root 0's bytes. */
+static int allreduce_short(struct MPIX_Hip_comm_s *c, const void *sendbuf, void *recvbuf, long count,
+                           size_t esz, int opidx, int elem, hipStream_t s, const char *fc)
+{
+    int p = c->size, q, nx = 0, rc = MPI_SUCCESS, mask;
+    size_t bytes = (size_t) count * esz, slot = (bytes + 255) & ~(size_t) 255;
+    xfer_t sends[MAX_XFER], recvs[MAX_XFER];
+    const void *ys[64];
+    char *scr = NULL, *own;
+    hipError_t e;
+    if (comm_scratch(c, (size_t) p * slot, &scr)) {
+        MPIR_Err_set_detail("%s: scratch allocation failed", fc);
+        return MPI_ERR_NO_MEM;
+    }
+    own = scr + (size_t) c->rank * slot;
+    e = hipMemcpyAsync(own, sendbuf == MPI_IN_PLACE ? recvbuf : sendbuf, bytes, hipMemcpyDeviceToDevice, s);
+    if (e != hipSuccess)
+        return hip_err(fc, e);
+    for (q = 0; q < p; q++) {
+        if (q == c->rank)
+            continue;
+        sends[nx].buf = own;
+        sends[nx].bytes = bytes;
+        sends[nx].peer = q;
+        recvs[nx].buf = scr + (size_t) q * slot;
+        recvs[nx].bytes = bytes;
+        recvs[nx++].peer = q;
+    }
+    if ((rc = group_exchange(c, sends, nx, recvs, nx, s)) != MPI_SUCCESS)
+        return rc;
+    if ((p & (p - 1)) == 0) {
+        /* power of two: the binomial tree IS the pairwise tree ((x0+x1)+(x2+x3))+... */
+        for (q = 0; q < p; q++)
+            ys[q] = scr + (size_t) q * slot;
+        return fold_tree(ys, p, recvbuf, count, opidx, elem, s, fc);
+    }
+    for (mask = 1; mask < p; mask <<= 1)
+        for (q = 0; q + mask < p; q += 2 * mask)
+            if ((rc = fold_step(scr + (size_t) (q + mask) * slot, scr + (size_t) q * slot, count, opidx, elem,
+                                s, fc)) != MPI_SUCCESS)
+                return rc;
+    e = hipMemcpyAsync(recvbuf, scr, bytes, hipMemcpyDeviceToDevice, s);
+    return e == hipSuccess ? MPI_SUCCESS : hip_err(fc, e);
+}
+
+/* MPI_Reduce_scatter_block, p*recvcount*size < 524288: recursive halving
+ * (reduce_scatter_block_intra_recursive_halving.c).  Block r is finished by
+ * newrank n = r/2 (r < 2*rem) or r - rem, as
+ *   Y_m = x_{2m+1} (+) x_{2m} for m < rem (pre-fold :163-195), else x_{m+rem};
+ *   tree ((z0+z1)+(z2+z3))+... over z_k = Y_{n ^ bitrev(k)} (halving :197-283,
+ *   mask = pof2/2 first, received data second).
+ * Here: one all-to-all of blocks (every rank gets x_q's block r from each q),
+ * the rem pre-fold steps, one fused tree combine into recvbuf. */
+static int reduce_scatter_block_short(struct MPIX_Hip_comm_s *c, const char *src, void *recvbuf, long recvcount,
+                                      size_t esz, int opidx, int elem, hipStream_t s, const char *fc)
+{
+    int p = c->size, q, nx = 0, rc = MPI_SUCCESS, pof2 = pof2_of(p), rem = p - pof2, bits = 0, n, k, m;
+    size_t nb = (size_t) recvcount * esz, slot = (nb + 255) & ~(size_t) 255;
+    xfer_t sends[MAX_XFER], recvs[MAX_XFER];
+    const void *ys[64];
+    char *scr = NULL;
+    hipError_t e;
+    while ((1 << bits) < pof2)
+        bits++;
+    if (comm_scratch(c, (size_t) p * slot, &scr)) {
+        MPIR_Err_set_detail("%s: scratch allocation failed", fc);
+        return MPI_ERR_NO_MEM;
+    }
+    /* own block into its slot: the pre-fold updates slots in place */
+    e = hipMemcpyAsync(scr + (size_t) c->rank * slot, src + (size_t) c->rank * nb, nb, hipMemcpyDeviceToDevice, s);
+    if (e != hipSuccess)
+        return hip_err(fc, e);
+    for (q = 0; q < p; q++) {
+        if (q == c->rank)
+            continue;
+        sends[nx].buf = (void *) (src + (size_t) q * nb);
+        sends[nx].bytes = nb;
+        sends[nx].peer = q;
+        recvs[nx].buf = scr + (size_t) q * slot;
+        recvs[nx].bytes = nb;
+        recvs[nx++].peer = q;
+    }
+    if ((rc = group_exchange(c, sends, nx, recvs, nx, s)) != MPI_SUCCESS)
+        return rc;
+    for (m = 0; m < rem; m++)
+        if ((rc = fold_step(scr + (size_t) (2 * m) * slot, scr + (size_t) (2 * m + 1) * slot, recvcount, opidx,
+                            elem, s, fc)) != MPI_SUCCESS)
+            return rc;
+    n = c->rank < 2 * rem ? c->rank / 2 : c->rank - rem;
+    for (k = 0; k < pof2; k++) {
+        int y = n ^ bitrev(k, bits);
+        ys[k] = scr + (size_t) (y < rem ? 2 * y + 1 : y + rem) * slot;
+    }
+    return fold_tree(ys, pof2, recvbuf, recvcount, opidx, elem, s, fc);
+}
+
 /* validation shared by both collectives (MPIR_ERRTEST_OP + check_dtype) */
 static int coll_check(const char *fc, const void *sendbuf, void *recvbuf, int count, MPI_Datatype dt, MPI_Op op,
                       MPIX_Hip_comm comm, int *elem)
@@ -472,10 +607,20 @@ int MPIX_Allreduce_hip(const void *sendbuf, void *recvbuf, int count, MPI_Dataty
         goto done_sync;
     }
 
-    /* ---- reference order (allreduce_intra_smp.c + reduce_intra_reduce_scatter_gather.c) */
+    /* ---- reference order (allreduce_intra_smp.c + MPIR_Reduce_intra_auto's choice) */
+    pof2 = pof2_of(p);
+    if (p == 1) {
+        if (sendbuf != MPI_IN_PLACE)
+            HIPTRY(hipMemcpyAsync(recvbuf, sendbuf, bytes, hipMemcpyDeviceToDevice, s));
+        goto done_sync;
+    }
+    if (bytes <= REDUCE_SHORT_MSG_SIZE || count < pof2) {
+        TRY(allreduce_short(c, sendbuf, recvbuf, count, esz, opidx, elem, s, fc));
+        goto done_sync;
+    }
+    /* long: reduce_intra_reduce_scatter_gather.c */
     if (sendbuf != MPI_IN_PLACE)
         HIPTRY(hipMemcpyAsync(recvbuf, sendbuf, bytes, hipMemcpyDeviceToDevice, s));
-    pof2 = pof2_of(p);
     rem = p - pof2;
     bits = 0;
     while ((1 << bits) < pof2)
@@ -625,7 +770,13 @@ int MPIX_Reduce_scatter_block_hip(const void *sendbuf, void *recvbuf, int recvco
         goto done_sync;
     }
 
-    /* ---- reference order (reduce_scatter_block_intra_pairwise.c:97-134):
+    /* ---- reference order: MPIR_Reduce_scatter_block_intra_auto (reduce_scatter_block.c:136-148)
+     * takes recursive halving below 524288 total bytes for commutative (all builtin) ops */
+    if (p > 1 && (size_t) p * nb < RSB_COMMUTATIVE_LONG_MSG_SIZE) {
+        TRY(reduce_scatter_block_short(c, src, recvbuf, recvcount, esz, opidx, elem, s, fc));
+        goto done_sync;
+    }
+    /* long: pairwise (reduce_scatter_block_intra_pairwise.c:97-134):
      * block r = ((x_r + x_{r-1}) + x_{r-2}) + ...; y_i = block r from rank r - i */
     if (comm_scratch(c, (size_t) (p > 1 ? p - 1 : 1) * nb + 256, &scr)) {
         MPIR_Err_set_detail("%s: scratch allocation failed", fc);

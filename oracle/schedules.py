@@ -16,6 +16,20 @@ summation order the GPU's fused schedule combines must reproduce bit for bit.
   allreduce_rsag          src/mpi/coll/allreduce/allreduce_intra_reduce_scatter_allgather.c:72-290
   reduce_scatter_block_pairwise
                           src/mpi/coll/reduce_scatter_block/reduce_scatter_block_intra_pairwise.c:75-134
+  reduce_binomial         src/mpi/coll/reduce/reduce_intra_binomial.c:93-140 (commutative op:
+                          lroot = root)
+  allreduce_smp_auto      allreduce_intra_smp.c with MPIR_Reduce_intra_auto's choice
+                          (reduce.c:214-225): reduce_scatter_gather when nbytes > 2048
+                          (MPIR_CVAR_REDUCE_SHORT_MSG_SIZE), builtin op and count >= pof2,
+                          else the binomial tree; then MPIR_Bcast
+  reduce_scatter_block_recursive_halving
+                          src/mpi/coll/reduce_scatter_block/
+                          reduce_scatter_block_intra_recursive_halving.c:143-300
+  reduce_scatter_block_auto
+                          MPIR_Reduce_scatter_block_intra_auto (reduce_scatter_block.c:136-148):
+                          builtin ops are commutative, so recursive halving below 524288
+                          total bytes (MPIR_CVAR_REDUCE_SCATTER_COMMUTATIVE_LONG_MSG_SIZE),
+                          pairwise from there on
 """
 from __future__ import annotations
 
@@ -159,3 +173,121 @@ def reduce_scatter_block_pairwise(rank_sendbufs: list[np.ndarray], recvcount: in
             tmp = send[src][r * nb:(r + 1) * nb].copy()
             _red(tmp, recv[r], recvcount, dt, op)
     return recv
+
+
+REDUCE_SHORT_MSG_SIZE = 2048            # reduce.c:14-17 (MPIR_CVAR_REDUCE_SHORT_MSG_SIZE)
+RSB_COMMUTATIVE_LONG_MSG_SIZE = 524288  # reduce_scatter.c:14-17
+
+
+def reduce_binomial(rank_bufs: list[np.ndarray], count: int, esz: int, dt: int, op: int,
+                    root: int = 0) -> np.ndarray:
+    """MPI_Reduce's binomial tree (reduce_intra_binomial.c:93-140), commutative op:
+    relrank r with bit `mask` clear receives the accumulation of relrank r|mask
+    and folds it in as the SECOND operand (MPIR_Reduce_local(tmp_buf, recvbuf)),
+    so recvbuf = recvbuf (+) tmp.  Returns the root's recvbuf."""
+    p = len(rank_bufs)
+    acc = [b.view(np.uint8).reshape(-1).copy() for b in rank_bufs]   # indexed by real rank
+    mask = 1
+    while mask < p:
+        for rel in range(0, p, 2 * mask):            # the ranks still receiving at this mask
+            src_rel = rel | mask
+            if src_rel < p:
+                r, src = (rel + root) % p, (src_rel + root) % p
+                tmp = acc[src].copy()                # src sent its finished accumulation
+                _red(tmp, acc[r], count, dt, op)
+        mask <<= 1
+    return acc[root]
+
+
+def allreduce_smp_auto(rank_bufs: list[np.ndarray], count: int, esz: int, dt: int, op: int) -> np.ndarray:
+    """MPI_Allreduce on one node with MPICH's algorithm choice: MPIR_Reduce to node
+    root 0 (reduce.c:214: reduce_scatter_gather if count*size > 2048 and
+    count >= pof2 for a builtin op, else binomial) followed by MPIR_Bcast."""
+    p = len(rank_bufs)
+    if p == 1:
+        return rank_bufs[0].view(np.uint8).reshape(-1).copy()
+    if count * esz > REDUCE_SHORT_MSG_SIZE and count >= _pof2(p):
+        return allreduce_smp(rank_bufs, count, esz, dt, op)
+    return reduce_binomial(rank_bufs, count, esz, dt, op, root=0)
+
+
+def reduce_scatter_block_recursive_halving(rank_sendbufs: list[np.ndarray], recvcount: int, esz: int,
+                                           dt: int, op: int) -> list[np.ndarray]:
+    """Each rank's recvbuf after MPI_Reduce_scatter_block's recursive halving
+    (reduce_scatter_block_intra_recursive_halving.c), step by step:
+      pre-fold :163-195   even r < 2*rem sends everything to r+1, which computes
+                          tmp_results = x_r (+) x_{r-1} (its own data first)
+      halving  :197-283   newrank n, mask = pof2/2 .. 1, partner n ^ mask; the lower
+                          newrank keeps the low half of [send_idx, last_idx); received
+                          data is folded in as the second operand
+      final    :285-300   every participant copies its block; odd r < 2*rem sends
+                          block r-1 back to r-1."""
+    p = len(rank_sendbufs)
+    nb = recvcount * esz
+    total = p * recvcount
+    res = [b.view(np.uint8).reshape(-1)[:p * nb].copy() for b in rank_sendbufs]   # tmp_results
+    pof2 = _pof2(p)
+    rem = p - pof2
+    newrank = [0] * p
+    for r in range(p):
+        if r < 2 * rem:
+            if r % 2 == 0:
+                newrank[r] = -1
+            else:
+                tmp = res[r - 1].copy()
+                _red(tmp, res[r], total, dt, op)
+                newrank[r] = r // 2
+        else:
+            newrank[r] = r - rem
+    newcnts = []
+    for i in range(pof2):
+        old_i = i * 2 + 1 if i < rem else i + rem
+        newcnts.append(2 * recvcount if old_i < 2 * rem else recvcount)
+    newdisps = [0] * pof2
+    for i in range(1, pof2):
+        newdisps[i] = newdisps[i - 1] + newcnts[i - 1]
+    real = {newrank[r]: r for r in range(p) if newrank[r] >= 0}
+    st = {r: [0, 0, pof2] for r in real.values()}     # send_idx, recv_idx, last_idx
+    mask = pof2 >> 1
+    while mask > 0:
+        plans = {}
+        for n, r in real.items():
+            s = st[r]
+            nd = n ^ mask
+            if n < nd:
+                s[0] = s[1] + mask
+                send_lo, send_hi, recv_lo, recv_hi = s[0], s[2], s[1], s[0]
+            else:
+                s[1] = s[0] + mask
+                send_lo, send_hi, recv_lo, recv_hi = s[0], s[1], s[1], s[2]
+            scnt = sum(newcnts[send_lo:send_hi])
+            lo = newdisps[send_lo] * esz if send_hi > send_lo else 0
+            plans[r] = (real[nd], res[r][lo:lo + scnt * esz].copy(), recv_lo, recv_hi)
+        for n, r in real.items():
+            peer, _, recv_lo, recv_hi = plans[r]
+            rcnt = sum(newcnts[recv_lo:recv_hi])
+            if rcnt:
+                lo = newdisps[recv_lo] * esz
+                data = plans[peer][1]
+                assert data.size == rcnt * esz
+                _red(data, res[r][lo:lo + rcnt * esz], rcnt, dt, op)
+            s = st[r]
+            s[0] = s[1]
+            s[2] = s[1] + mask
+        mask >>= 1
+    out = [None] * p
+    for r in range(p):
+        if newrank[r] >= 0:
+            out[r] = res[r][r * nb:(r + 1) * nb].copy()
+    for r in range(0, 2 * rem, 2):
+        out[r] = res[r + 1][r * nb:(r + 1) * nb].copy()
+    return out
+
+
+def reduce_scatter_block_auto(rank_sendbufs: list[np.ndarray], recvcount: int, esz: int, dt: int,
+                              op: int) -> list[np.ndarray]:
+    """MPI_Reduce_scatter_block with MPICH's algorithm choice for a builtin
+    (commutative) op (reduce_scatter_block.c:136-148)."""
+    if len(rank_sendbufs) * recvcount * esz < RSB_COMMUTATIVE_LONG_MSG_SIZE:
+        return reduce_scatter_block_recursive_halving(rank_sendbufs, recvcount, esz, dt, op)
+    return reduce_scatter_block_pairwise(rank_sendbufs, recvcount, esz, dt, op)

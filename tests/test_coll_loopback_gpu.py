@@ -58,7 +58,7 @@ def test_allreduce_reference_order(mpi, orc, cuda, t, op, p, inplace):
             rng = np.random.default_rng(seed)
             xs = [T.to_bytes(T.gen(t, count, rng, op)) for _ in range(p)]
             if p > 1:
-                want = S.allreduce_smp(xs, count, esz, mpi.DATATYPES[t], mpi.OPS[op])
+                want = S.allreduce_smp_auto(xs, count, esz, mpi.DATATYPES[t], mpi.OPS[op])
             else:
                 want = xs[0]
             send = [torch.from_numpy(x.copy()).cuda() for x in xs]
@@ -84,7 +84,7 @@ def test_allreduce_reference_order(mpi, orc, cuda, t, op, p, inplace):
 @pytest.mark.parametrize("t,op", [("MPIX_C_FLOAT16", "MPI_SUM"), ("MPI_FLOAT", "MPI_SUM"), ("MPI_INT64_T", "MPI_PROD"),
                                   ("MPI_UNSIGNED", "MPI_BAND"), ("MPI_FLOAT", "MPI_MIN"),
                                   ("MPI_LONG_DOUBLE_INT", "MPI_MINLOC")])
-@pytest.mark.parametrize("p", [1, 2, 3, 8])
+@pytest.mark.parametrize("p", [1, 2, 3, 5, 6, 8])
 @pytest.mark.parametrize("inplace", [False, True])
 def test_reduce_scatter_block_reference_order(mpi, orc, cuda, t, op, p, inplace):
     from oracle import schedules as S
@@ -95,7 +95,7 @@ def test_reduce_scatter_block_reference_order(mpi, orc, cuda, t, op, p, inplace)
         for recvcount, seed in ((2053, p), ((1 << 18) + 1, 3 * p)):
             rng = np.random.default_rng(seed)
             xs = [T.to_bytes(T.gen(t, recvcount * p, rng, op)) for _ in range(p)]
-            want = S.reduce_scatter_block_pairwise(xs, recvcount, esz, mpi.DATATYPES[t], mpi.OPS[op])
+            want = S.reduce_scatter_block_auto(xs, recvcount, esz, mpi.DATATYPES[t], mpi.OPS[op])
             send = [torch.from_numpy(x.copy()).cuda() for x in xs]
             recv = [s.clone() if inplace else torch.zeros(recvcount * esz, dtype=torch.uint8, device="cuda")
                     for s in send]
@@ -115,6 +115,55 @@ def test_reduce_scatter_block_reference_order(mpi, orc, cuda, t, op, p, inplace)
     finally:
         for c in comms:
             mpi.comm_free(c)
+
+
+SWITCH = [("MPI_FLOAT", "MPI_SUM"), ("MPI_DOUBLE", "MPI_MAX"), ("MPIX_C_FLOAT16", "MPI_MIN")]
+
+
+@pytest.mark.parametrize("t,op", SWITCH, ids=[f"{t}-{o}" for t, o in SWITCH])
+@pytest.mark.parametrize("p", [6, 8])
+def test_algorithm_switch_points(mpi, orc, cuda, t, op, p):
+    """Both sides of MPICH's size thresholds: Allreduce binomial <= 2048 B <
+    reduce-scatter-gather (reduce.c:214); Reduce_scatter_block recursive halving
+    < 524288 total bytes <= pairwise (reduce_scatter_block.c:136-141)."""
+    from oracle import schedules as S
+    torch = cuda
+    esz = T.elem_size(t)
+    dt, o = mpi.DATATYPES[t], mpi.OPS[op]
+    comms = mpi.comm_create_loopback(p)
+    try:
+        for count in (2048 // esz, 2048 // esz + 1):
+            rng = np.random.default_rng(count + p)
+            xs = [T.to_bytes(T.gen(t, count, rng, op)) for _ in range(p)]
+            want = S.allreduce_smp_auto(xs, count, esz, dt, o)
+            send = [torch.from_numpy(x.copy()).cuda() for x in xs]
+            recv = [torch.zeros_like(x) for x in send]
+            torch.cuda.synchronize()
+            run_ranks(lambda r: _ok(mpi, mpi.allreduce(send[r].data_ptr(), recv[r].data_ptr(), count, dt, o,
+                                                       comms[r], mpi.MPIX_HIP_ALG_REFERENCE_ORDER)), p)
+            torch.cuda.synchronize()
+            for r in range(p):
+                assert same(recv[r].cpu().numpy(), want, t), f"allreduce count {count} rank {r}"
+        first_long = -(-S.RSB_COMMUTATIVE_LONG_MSG_SIZE // (p * esz))
+        for rc in (first_long - 1, first_long):
+            rng = np.random.default_rng(rc + p)
+            xs = [T.to_bytes(T.gen(t, rc * p, rng, op)) for _ in range(p)]
+            want = S.reduce_scatter_block_auto(xs, rc, esz, dt, o)
+            send = [torch.from_numpy(x.copy()).cuda() for x in xs]
+            recv = [torch.zeros(rc * esz, dtype=torch.uint8, device="cuda") for _ in range(p)]
+            torch.cuda.synchronize()
+            run_ranks(lambda r: _ok(mpi, mpi.reduce_scatter_block(send[r].data_ptr(), recv[r].data_ptr(), rc, dt,
+                                                                  o, comms[r], mpi.MPIX_HIP_ALG_REFERENCE_ORDER)), p)
+            torch.cuda.synchronize()
+            for r in range(p):
+                assert same(recv[r].cpu().numpy(), want[r], t), f"reduce_scatter_block recvcount {rc} rank {r}"
+    finally:
+        for c in comms:
+            mpi.comm_free(c)
+
+
+def _ok(mpi, rc):
+    assert rc == 0, mpi.error_string(rc)
 
 
 def test_collective_validation(mpi, cuda):

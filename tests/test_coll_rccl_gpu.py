@@ -89,7 +89,7 @@ def test_allreduce_over_rccl(mpi, orc, cuda, size):
     for k, (t, op, count, alg) in enumerate(cases):
         xs = [res[r][3][k][1] for r in range(size)]
         esz = T.elem_size(t)
-        want = S.allreduce_smp(xs, count, esz, mpi.DATATYPES[t], mpi.OPS[op]) if size > 1 else xs[0]
+        want = S.allreduce_smp_auto(xs, count, esz, mpi.DATATYPES[t], mpi.OPS[op]) if size > 1 else xs[0]
         for r in range(size):
             rc, _, got = res[r][3][k]
             assert rc == 0
