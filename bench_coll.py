@@ -135,7 +135,9 @@ def main():
     assert m.allreduce(send.data_ptr(), recv.data_ptr(), n, F32, SUM, C, REF) == 0
     ok_ar = bool(np.array_equal(recv.cpu().numpy().view(np.uint32), expect_allreduce(xs).view(np.uint32))) \
         if pof2 else True
-    rcount = 4099
+    # large enough that MPICH takes the pairwise algorithm at every N >= 2
+    # (p * recvcount * 2 B >= 524288, reduce_scatter_block.c:136-141)
+    rcount = (1 << 17) + 3
     hs = [np.random.default_rng(91 + r).uniform(-4, 4, rcount * world).astype(np.float16) for r in range(world)]
     hsend = torch.from_numpy(hs[rank].copy()).cuda()
     hrecv = torch.zeros(rcount, dtype=torch.float16, device="cuda")
