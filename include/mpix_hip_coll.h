@@ -41,6 +41,10 @@ extern "C" {
 
 typedef struct MPIX_Hip_comm_s *MPIX_Hip_comm;
 
+#ifndef MPI_ERR_ROOT
+#define MPI_ERR_ROOT 7      /* mpi.h.in:792 */
+#endif
+
 #define MPIX_HIP_UNIQUE_ID_BYTES 128
 #define MPIX_HIP_ALG_AUTO 0
 #define MPIX_HIP_ALG_REFERENCE_ORDER 1
@@ -56,6 +60,13 @@ int MPIX_Hip_comm_size(MPIX_Hip_comm comm, int *size);
 /* MPI_Allreduce semantics (sendbuf may be MPI_IN_PLACE). */
 int MPIX_Allreduce_hip(const void *sendbuf, void *recvbuf, int count, MPI_Datatype datatype, MPI_Op op,
                        MPIX_Hip_comm comm, int algorithm, void *hip_stream);
+/* MPI_Reduce semantics (reduce.c:742; MPI_IN_PLACE at the root only; recvbuf
+ * significant at the root only).  Reference order: reduce_intra_smp.c ->
+ * MPIR_Reduce_intra_auto on the node (binomial tree rooted at `root` for
+ * count*size <= 2048 or count < pof2, else reduce-scatter + gather);
+ * MPIX_HIP_ALG_RCCL: ncclReduce. */
+int MPIX_Reduce_hip(const void *sendbuf, void *recvbuf, int count, MPI_Datatype datatype, MPI_Op op, int root,
+                    MPIX_Hip_comm comm, int algorithm, void *hip_stream);
 /* MPI_Reduce_scatter_block semantics (sendbuf may be MPI_IN_PLACE). */
 int MPIX_Reduce_scatter_block_hip(const void *sendbuf, void *recvbuf, int recvcount, MPI_Datatype datatype,
                                   MPI_Op op, MPIX_Hip_comm comm, int algorithm, void *hip_stream);

@@ -19,13 +19,24 @@ namespace {
 
 typedef hipError_t (*launch_fn)(const void *, void *, uint64_t, hipStream_t);
 
-struct Entry { launch_fn fn; };
+typedef hipError_t (*any_fn)(const void *const *, int, int, void *, uint64_t, hipStream_t);
+
+// g_table: the single-operand MPIR_Reduce_local kernel per (op, element class);
+// any: the one-pass n-operand combine of the same pair (MPIR_Hip_combine's
+// general path).  REPLACE has no n-operand form (its fold is the last operand).
+struct Entry { launch_fn fn; any_fn any; };
 Entry g_table[MPIR_HIP_NOPS][MPIR_HIP_NELEMS];
 
 template <class Op, class T>
-void reg(int op, int elem) { g_table[op][elem].fn = &launch_reduce<Op, T>; }
+void reg(int op, int elem) {
+    g_table[op][elem].fn = &launch_reduce<Op, T>;
+    if constexpr (!__is_same(Op, OpReplace)) g_table[op][elem].any = &launch_combine_any<Op, T>;
+}
 template <class Op, class T, int EPL = 2>
-void reg_wide(int op, int elem) { g_table[op][elem].fn = &launch_reduce_wide<Op, T, EPL>; }
+void reg_wide(int op, int elem) {
+    g_table[op][elem].fn = &launch_reduce_wide<Op, T, EPL>;
+    g_table[op][elem].any = &launch_combine_any<Op, T>;
+}
 
 // Integer element classes and their device types.
 #define FOR_INTS(X) \
@@ -333,61 +344,32 @@ int MPIR_Hip_combine(const void *const *inbufs, int n, void *outbuf, uint64_t co
         const bool fused = g_multi[op][elem][0][0] != nullptr;
         if (n == 1) {
             if (outbuf != inbufs[0]) e = hipMemcpyAsync(outbuf, inbufs[0], count * esz, hipMemcpyDeviceToDevice, s);
-        } else if (order == MPIR_HIP_ORDER_TREE) {
-            if (fused && n <= 8) {
-                e = g_multi[op][elem][0][n == 2 ? 0 : (n == 4 ? 1 : 2)](inbufs, outbuf, count, s);
-            } else if (!g_table[op][elem].fn) {
-                rc = MPIR_HIP_ENOKERNEL;
-            } else {
-                // Level by level with the single-operand kernel, same association:
-                // v_j = v_j (+) v_{j+step} (left operand = v_j).  v_0 lives in
-                // outbuf, v_j (j > 0 even) in device scratch.
-                const uint64_t bytes = count * esz, slot = (bytes + 255) & ~(uint64_t)255;
-                const uint64_t unit = (op == MPIR_HIP_OP_REPLACE) ? 1 : esz;
-                // stream-ordered temporaries (hipMallocAsync): safe when calls on
-                // different streams overlap
-                char *scr = nullptr;
-                if (n > 2) e = hipMallocAsync((void **)&scr, (size_t)(n / 2 - 1) * slot, s);
-                void *v[64];
-                for (int j = 0; j < n && rc == MPIR_HIP_OK; ++j) v[j] = const_cast<void *>(inbufs[j]);
-                for (int step = 1; step < n && rc == MPIR_HIP_OK && e == hipSuccess; step *= 2) {
-                    for (int j = 0; j < n && e == hipSuccess; j += 2 * step) {
-                        if (step == 1) {   // first level: copy y_j into its accumulator slot
-                            void *dst = j == 0 ? outbuf : scr + (uint64_t)(j / 2 - 1) * slot;
-                            if (dst != v[j]) e = hipMemcpyAsync(dst, v[j], bytes, hipMemcpyDeviceToDevice, s);
-                            v[j] = dst;
-                        }
-                        if (e == hipSuccess) e = g_table[op][elem].fn(v[j + step], v[j], bytes / unit, s);
-                    }
-                }
-                if (scr) {
-                    const hipError_t ef = hipFreeAsync(scr, s);
-                    if (e == hipSuccess) e = ef;
-                }
-            }
-        } else {
+        } else if (op == MPIR_HIP_OP_REPLACE) {
+            // a fold of REPLACE in either order is the last operand
+            if (outbuf != inbufs[n - 1])
+                e = hipMemcpyAsync(outbuf, inbufs[n - 1], count * esz, hipMemcpyDeviceToDevice, s);
+        } else if (order == MPIR_HIP_ORDER_TREE && fused && n <= 8) {
+            e = g_multi[op][elem][0][n == 2 ? 0 : (n == 4 ? 1 : 2)](inbufs, outbuf, count, s);
+        } else if (order == MPIR_HIP_ORDER_CHAIN && fused) {
             // CHAIN: acc = y0; fold y1..y_{n-1} in order.  Greedy chunks of
             // P = 8/4/2 operands, each chunk's first operand the running acc.
             const void *acc = inbufs[0];
             int i = 1;
-            while (e == hipSuccess && rc == MPIR_HIP_OK && i < n) {
+            while (e == hipSuccess && i < n) {
                 const int left = n - i;
-                if (fused) {
-                    const int P = left >= 7 ? 8 : (left >= 3 ? 4 : 2);
-                    const void *ops[8];
-                    ops[0] = acc;
-                    for (int j = 1; j < P; ++j) ops[j] = inbufs[i + j - 1];
-                    e = g_multi[op][elem][1][P == 2 ? 0 : (P == 4 ? 1 : 2)](ops, outbuf, count, s);
-                    i += P - 1;
-                } else {
-                    if (acc != outbuf) e = hipMemcpyAsync(outbuf, acc, count * esz, hipMemcpyDeviceToDevice, s);
-                    const uint64_t unit = (op == MPIR_HIP_OP_REPLACE) ? 1 : esz;
-                    if (e == hipSuccess) e = g_table[op][elem].fn ? g_table[op][elem].fn(inbufs[i], outbuf, count * esz / unit, s)
-                                                                 : hipErrorInvalidValue;
-                    i += 1;
-                }
+                const int P = left >= 7 ? 8 : (left >= 3 ? 4 : 2);
+                const void *ops[8];
+                ops[0] = acc;
+                for (int j = 1; j < P; ++j) ops[j] = inbufs[i + j - 1];
+                e = g_multi[op][elem][1][P == 2 ? 0 : (P == 4 ? 1 : 2)](ops, outbuf, count, s);
+                i += P - 1;
                 acc = outbuf;
             }
+        } else if (g_table[op][elem].any) {
+            // one pass, no temporaries (k_combine_any)
+            e = g_table[op][elem].any(inbufs, n, order == MPIR_HIP_ORDER_TREE, outbuf, count, s);
+        } else {
+            rc = MPIR_HIP_ENOKERNEL;
         }
         if (e != hipSuccess) rc = set_err(e, "combine launch");
         if (rc == MPIR_HIP_OK && sync) rc = wait_stream(dev, s);

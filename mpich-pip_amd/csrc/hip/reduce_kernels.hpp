@@ -410,6 +410,74 @@ hipError_t launch_combine_pu(const void *const *ins, void *out_, uint64_t count,
     return hipGetLastError();
 }
 
+// Any (op, element class), any n <= 64, either order, in ONE pass with no
+// device temporaries: the combine for the (op, type) pairs the fused
+// k_combine_multi is not instantiated for (logical / bitwise ops, MAXLOC /
+// MINLOC pairs, complex PROD, long double) and for n > 8.  Element-granular
+// and grid-stride; the tree is evaluated left to right with a per-thread
+// stack (a binary counter of partial results), which is the association
+// ((y0+y1)+(y2+y3))+... with the earlier partial always the left operand.
+// out may alias in[0]: every input of element i is read before out[i] is written.
+constexpr int kMaxAnyOperands = 64;
+struct AnyArgs {
+    const char *in[kMaxAnyOperands];
+    char *out;
+    int n;
+    int tree;
+};
+
+template <class Op, class T>
+__global__ __launch_bounds__(kThreads) void k_combine_any(AnyArgs a, uint64_t count) {
+    Op op;
+    const uint64_t stride = (uint64_t)gridDim.x * kThreads;
+    for (uint64_t i = (uint64_t)blockIdx.x * kThreads + threadIdx.x; i < count; i += stride) {
+        const uint64_t off = i * sizeof(T);
+        T acc;
+        __builtin_memcpy(&acc, a.in[0] + off, sizeof(T));
+        if (!a.tree) {
+            for (int j = 1; j < a.n; ++j) {
+                T v;
+                __builtin_memcpy(&v, a.in[j] + off, sizeof(T));
+                acc = op(acc, v);
+            }
+        } else {
+            T st[7];
+            int lv[7];
+            int sp = 0;
+            for (int j = 0; j < a.n; ++j) {
+                T v = acc;
+                if (j) __builtin_memcpy(&v, a.in[j] + off, sizeof(T));
+                int l = 0;
+                while (sp > 0 && lv[sp - 1] == l) {
+                    v = op(st[sp - 1], v);
+                    --sp;
+                    ++l;
+                }
+                st[sp] = v;
+                lv[sp] = l;
+                ++sp;
+            }
+            acc = st[0];
+        }
+        __builtin_memcpy(a.out + off, &acc, sizeof(T));
+    }
+}
+
+template <class Op, class T>
+hipError_t launch_combine_any(const void *const *ins, int n, int tree, void *out, uint64_t count, hipStream_t s) {
+    if (n < 1 || n > kMaxAnyOperands || (tree && (n & (n - 1)))) return hipErrorInvalidValue;
+    AnyArgs a;
+    for (int j = 0; j < kMaxAnyOperands; ++j) a.in[j] = j < n ? static_cast<const char *>(ins[j]) : nullptr;
+    a.out = static_cast<char *>(out);
+    a.n = n;
+    a.tree = tree;
+    uint64_t grid = (count + kThreads - 1) / kThreads;
+    if (grid > 8192) grid = 8192;
+    if (grid == 0) grid = 1;
+    hipLaunchKernelGGL((k_combine_any<Op, T>), dim3((unsigned)grid), dim3(kThreads), 0, s, a, count);
+    return hipGetLastError();
+}
+
 template <class Op, class T, int P, bool TREE>
 hipError_t launch_combine_p(const void *const *ins, void *out_, uint64_t count, hipStream_t s) {
     return launch_combine_pu<Op, T, P, TREE, (P >= 8 ? 1 : (P >= 4 ? 2 : 4))>(ins, out_, count, s);

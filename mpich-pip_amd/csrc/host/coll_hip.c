@@ -50,6 +50,8 @@ static struct {
     ncclResult_t (*AllReduce)(const void *, void *, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t, hipStream_t);
     ncclResult_t (*ReduceScatter)(const void *, void *, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t,
                                   hipStream_t);
+    ncclResult_t (*Reduce)(const void *, void *, size_t, ncclDataType_t, ncclRedOp_t, int, ncclComm_t,
+                           hipStream_t);
     ncclResult_t (*Send)(const void *, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t);
     ncclResult_t (*Recv)(void *, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t);
     ncclResult_t (*GroupStart)(void);
@@ -76,6 +78,7 @@ static int rccl_load(void)
         SYM(CommDestroy, "ncclCommDestroy");
         SYM(AllReduce, "ncclAllReduce");
         SYM(ReduceScatter, "ncclReduceScatter");
+        SYM(Reduce, "ncclReduce");
         SYM(Send, "ncclSend");
         SYM(Recv, "ncclRecv");
         SYM(GroupStart, "ncclGroupStart");
@@ -84,7 +87,7 @@ static int rccl_load(void)
 #undef SYM
     }
     rccl.loaded = (rccl.so && rccl.GetUniqueId && rccl.CommInitRank && rccl.Send && rccl.Recv &&
-                   rccl.GroupStart && rccl.GroupEnd && rccl.AllReduce && rccl.ReduceScatter) ? 1 : -1;
+                   rccl.GroupStart && rccl.GroupEnd && rccl.AllReduce && rccl.ReduceScatter && rccl.Reduce) ? 1 : -1;
     pthread_mutex_unlock(&rccl_lock);
     return rccl.loaded > 0;
 }
@@ -569,18 +572,88 @@ static int want_rccl(struct MPIX_Hip_comm_s *c, int algorithm, int elem, int opi
         MPIR_Err_set_detail("%s: %s", #x, hipGetErrorString(e_)); rc = MPI_ERR_OTHER; goto done; } } while (0)
 #define TRY(x) do { if ((rc = (x)) != MPI_SUCCESS) goto done; } while (0)
 
+/* The reduce-scatter phase of reduce_intra_reduce_scatter_gather.c on `work`
+ * (count elements, this rank's contribution): the non-power-of-two pre-fold
+ * (:138-170: odd r < 2*rem sends everything to r-1, which computes x_r (+) x_{r+1}),
+ * then the recursive halving (:186-249) as ONE all-to-all of blocks and ONE
+ * fused tree combine: newrank n owns block bitrev(n), reduced as
+ * ((y0+y1)+(y2+y3))+... with y_j = the block from newrank n ^ j.
+ * `scr` holds (pof2-1) * cnts[0] elements + count elements + 256 bytes.
+ * Returns this rank's newrank in *newrank (-1: excluded by the pre-fold). */
+static int rsg_phase(struct MPIX_Hip_comm_s *c, char *work, long count, size_t esz, int opidx, int elem,
+                     hipStream_t s, const char *fc, char *scr, const long *cnts, const long *disps, int *newrank)
+{
+    int p = c->size, pof2 = pof2_of(p), rem = p - pof2, bits = 0, nsend = 0, nrecv = 0, rc, i;
+    size_t bytes = (size_t) count * esz, maxblk = (size_t) cnts[0];
+    xfer_t sends[MAX_XFER], recvs[MAX_XFER];
+    while ((1 << bits) < pof2)
+        bits++;
+    /* pre-fold; every rank takes part in the transfer group (empty for ranks >= 2*rem) */
+    if (rem > 0 && c->rank >= 2 * rem)
+        if ((rc = group_exchange(c, NULL, 0, NULL, 0, s)) != MPI_SUCCESS)
+            return rc;
+    if (c->rank < 2 * rem) {
+        if (c->rank % 2) {
+            xfer_t x = { work, bytes, c->rank - 1 };
+            if ((rc = group_exchange(c, &x, 1, NULL, 0, s)) != MPI_SUCCESS)
+                return rc;
+            *newrank = -1;
+        } else {
+            char *tmp = scr + (size_t) (pof2 > 1 ? pof2 - 1 : 1) * maxblk * esz;
+            xfer_t x = { tmp, bytes, c->rank + 1 };
+            if ((rc = group_exchange(c, NULL, 0, &x, 1, s)) != MPI_SUCCESS)
+                return rc;
+            if ((rc = fold_step(tmp, work, count, opidx, elem, s, fc)) != MPI_SUCCESS)
+                return rc;
+            *newrank = c->rank / 2;
+        }
+    } else
+        *newrank = c->rank - rem;
+
+    /* all-to-all of blocks: the owner receives y_j into scratch slot j-1 */
+    if (*newrank >= 0 && pof2 > 1) {
+        int n = *newrank, mb = bitrev(n, bits), m;
+        const void *ys[64];
+        for (m = 0; m < pof2; m++) {
+            int real, b;
+            if (m == n)
+                continue;
+            real = m < rem ? 2 * m : m + rem;
+            b = bitrev(m, bits);
+            sends[nsend].buf = work + disps[b] * esz;
+            sends[nsend].bytes = (size_t) cnts[b] * esz;
+            sends[nsend++].peer = real;
+            recvs[nrecv].buf = scr + (size_t) ((n ^ m) - 1) * maxblk * esz;
+            recvs[nrecv].bytes = (size_t) cnts[mb] * esz;
+            recvs[nrecv++].peer = real;
+        }
+        if ((rc = group_exchange(c, sends, nsend, recvs, nrecv, s)) != MPI_SUCCESS)
+            return rc;
+        ys[0] = work + disps[mb] * esz;
+        for (i = 1; i < pof2; i++)
+            ys[i] = scr + (size_t) (i - 1) * maxblk * esz;
+        if (cnts[mb] && (rc = fold_tree(ys, pof2, work + disps[mb] * esz, cnts[mb], opidx, elem, s, fc)))
+            return rc;
+    } else if (pof2 > 1) {
+        /* excluded rank: matches the group call of the participants (no transfers) */
+        if ((rc = group_exchange(c, NULL, 0, NULL, 0, s)) != MPI_SUCCESS)
+            return rc;
+    }
+    return MPI_SUCCESS;
+}
+
 /* ------------------------------------------------------------ Allreduce */
 int MPIX_Allreduce_hip(const void *sendbuf, void *recvbuf, int count, MPI_Datatype datatype, MPI_Op op,
                        MPIX_Hip_comm comm, int algorithm, void *hip_stream)
 {
     static const char *fc = "MPIX_Allreduce_hip";
     struct MPIX_Hip_comm_s *c = comm;
-    int elem = 0, opidx = op & 0xf, rc, p, pof2, rem, newrank, bits, i;
+    int elem = 0, opidx = op & 0xf, rc, p, pof2, rem, newrank = -1, bits, i;
     size_t esz, bytes;
     hipStream_t s;
     ncclDataType_t nt;
     ncclRedOp_t no;
-    long cnts[64] = {0}, disps[64] = {0}, maxblk;
+    long cnts[64] = {0}, disps[64] = {0};
     xfer_t sends[MAX_XFER], recvs[MAX_XFER];
     int nsend = 0, nrecv = 0, cur = 0;
     char *scr = NULL;
@@ -618,7 +691,7 @@ int MPIX_Allreduce_hip(const void *sendbuf, void *recvbuf, int count, MPI_Dataty
         TRY(allreduce_short(c, sendbuf, recvbuf, count, esz, opidx, elem, s, fc));
         goto done_sync;
     }
-    /* long: reduce_intra_reduce_scatter_gather.c */
+    /* long: reduce_intra_reduce_scatter_gather.c's reduce-scatter on recvbuf */
     if (sendbuf != MPI_IN_PLACE)
         HIPTRY(hipMemcpyAsync(recvbuf, sendbuf, bytes, hipMemcpyDeviceToDevice, s));
     rem = p - pof2;
@@ -626,72 +699,12 @@ int MPIX_Allreduce_hip(const void *sendbuf, void *recvbuf, int count, MPI_Dataty
     while ((1 << bits) < pof2)
         bits++;
     cnts_disps(count, pof2, cnts, disps);
-    maxblk = cnts[0];
-    if (comm_scratch(c, (size_t) (pof2 > 1 ? pof2 - 1 : 1) * (size_t) maxblk * esz + bytes + 256, &scr)) {
+    if (comm_scratch(c, (size_t) (pof2 - 1) * (size_t) cnts[0] * esz + bytes + 256, &scr)) {
         MPIR_Err_set_detail("%s: scratch allocation failed", fc);
         rc = MPI_ERR_NO_MEM;
         goto done;
     }
-    /* pre-fold (reduce_intra_reduce_scatter_gather.c:138-170); every rank takes
-     * part in the transfer group (empty for ranks >= 2*rem) */
-    if (rem > 0 && c->rank >= 2 * rem)
-        TRY(group_exchange(c, NULL, 0, NULL, 0, s));
-    if (c->rank < 2 * rem) {
-        if (c->rank % 2) {
-            xfer_t x = { recvbuf, bytes, c->rank - 1 };
-            TRY(group_exchange(c, &x, 1, NULL, 0, s));
-            newrank = -1;
-        } else {
-            char *tmp = scr + (size_t) (pof2 > 1 ? pof2 - 1 : 1) * (size_t) maxblk * esz;
-            xfer_t x = { tmp, bytes, c->rank + 1 };
-            TRY(group_exchange(c, NULL, 0, &x, 1, s));
-            rc = MPIR_Hip_reduce(tmp, recvbuf, (uint64_t) count, opidx, elem, s, 0);
-            if (rc) {
-                MPIR_Op_report_hip_error(fc, rc);
-                rc = MPI_ERR_OTHER;
-                goto done;
-            }
-            newrank = c->rank / 2;
-        }
-    } else
-        newrank = c->rank - rem;
-
-    /* all-to-all of blocks: newrank n owns block bitrev(n) (recursive halving,
-     * :186-249); the owner receives y_j = block from newrank n ^ j into slot j-1 */
-    if (newrank >= 0 && pof2 > 1) {
-        int mb = bitrev(newrank, bits), m;
-        const void *ys[64];
-        nsend = nrecv = 0;
-        for (m = 0; m < pof2; m++) {
-            int real, b;
-            if (m == newrank)
-                continue;
-            real = m < rem ? 2 * m : m + rem;
-            b = bitrev(m, bits);
-            sends[nsend].buf = (char *) recvbuf + disps[b] * esz;
-            sends[nsend].bytes = (size_t) cnts[b] * esz;
-            sends[nsend++].peer = real;
-            recvs[nrecv].buf = scr + (size_t) ((newrank ^ m) - 1) * (size_t) maxblk * esz;
-            recvs[nrecv].bytes = (size_t) cnts[mb] * esz;
-            recvs[nrecv++].peer = real;
-        }
-        TRY(group_exchange(c, sends, nsend, recvs, nrecv, s));
-        ys[0] = (char *) recvbuf + disps[mb] * esz;
-        for (i = 1; i < pof2; i++)
-            ys[i] = scr + (size_t) (i - 1) * (size_t) maxblk * esz;
-        if (cnts[mb]) {
-            rc = MPIR_Hip_combine(ys, pof2, (char *) recvbuf + disps[mb] * esz, (uint64_t) cnts[mb], opidx, elem,
-                                  MPIR_HIP_ORDER_TREE, s, 0);
-            if (rc) {
-                MPIR_Op_report_hip_error(fc, rc);
-                rc = MPI_ERR_OTHER;
-                goto done;
-            }
-        }
-    } else if (newrank < 0 && pof2 > 1) {
-        /* excluded rank: matches the group call of the participants (no transfers) */
-        TRY(group_exchange(c, NULL, 0, NULL, 0, s));
-    }
+    TRY(rsg_phase(c, recvbuf, count, esz, opidx, elem, s, fc, scr, cnts, disps, &newrank));
 
     /* allgather of the reduced blocks to every rank (the gather + MPIR_Bcast of
      * allreduce_intra_smp.c move data only) */
@@ -714,8 +727,150 @@ int MPIX_Allreduce_hip(const void *sendbuf, void *recvbuf, int count, MPI_Dataty
         recvs[nrecv].bytes = (size_t) cnts[b] * esz;
         recvs[nrecv++].peer = real;
     }
-    if (p > 1)
-        TRY(group_exchange(c, sends, nsend, recvs, nrecv, s));
+    TRY(group_exchange(c, sends, nsend, recvs, nrecv, s));
+
+  done_sync:
+    if (rc == MPI_SUCCESS && !hip_stream)
+        HIPTRY(hipStreamSynchronize(s));
+  done:
+    if (cur != c->device)
+        (void) hipSetDevice(cur);
+    return rc ? MPIR_Err_return(fc, rc) : MPI_SUCCESS;
+}
+
+/* ------------------------------------------------------------ Reduce
+ * MPI_Reduce on one node: MPIR_Reduce_intra_smp (reduce_intra_smp.c) reduces
+ * to the root over node_comm with MPIR_Reduce_intra_auto (reduce.c:170-225):
+ *   count*size <= 2048 or count < pof2: binomial tree rooted at `root`
+ *       (reduce_intra_binomial.c:93-140, commutative: relrank = rank - root);
+ *       here a gather to the root, which folds the relranks in binomial order;
+ *   else reduce_intra_reduce_scatter_gather.c: the reduce-scatter phase of the
+ *       Allreduce (block values do not depend on the root), then the owners'
+ *       blocks are gathered to the root. */
+int MPIX_Reduce_hip(const void *sendbuf, void *recvbuf, int count, MPI_Datatype datatype, MPI_Op op, int root,
+                    MPIX_Hip_comm comm, int algorithm, void *hip_stream)
+{
+    static const char *fc = "MPIX_Reduce_hip";
+    struct MPIX_Hip_comm_s *c = comm;
+    int elem = 0, opidx = op & 0xf, rc, p, pof2, rem, newrank = -1, bits, i, isroot, cur = 0;
+    size_t esz, bytes, slot;
+    hipStream_t s;
+    ncclDataType_t nt;
+    ncclRedOp_t no;
+    long cnts[64] = {0}, disps[64] = {0};
+    xfer_t sends[MAX_XFER], recvs[MAX_XFER];
+    int nsend = 0, nrecv = 0;
+    char *scr = NULL, *work;
+    const void *own;
+
+    if (comm && (root < 0 || root >= comm->size)) {
+        MPIR_Err_set_detail("%s: Invalid root (value given was %d)", fc, root);
+        return MPIR_Err_return(fc, MPI_ERR_ROOT);
+    }
+    isroot = comm && comm->rank == root;
+    if (comm && !isroot && sendbuf == MPI_IN_PLACE && count > 0) {
+        MPIR_Err_set_detail("%s: MPI_IN_PLACE is only valid at the root", fc);
+        return MPIR_Err_return(fc, MPI_ERR_BUFFER);
+    }
+    /* recvbuf is significant at the root only (the alias check with it too) */
+    rc = coll_check(fc, sendbuf, isroot ? recvbuf : NULL, count, datatype, op, comm, &elem);
+    if (rc)
+        return MPIR_Err_return(fc, rc);
+    if (count == 0)
+        return MPI_SUCCESS;
+    if (hipGetDevice(&cur) == hipSuccess && cur != c->device)
+        (void) hipSetDevice(c->device);
+    s = hip_stream ? (hipStream_t) hip_stream : c->stream;
+    esz = MPIR_Hip_elem_size(elem);
+    bytes = (size_t) count * esz;
+    p = c->size;
+    own = sendbuf == MPI_IN_PLACE ? recvbuf : sendbuf;
+
+    if (want_rccl(c, algorithm, elem, opidx, &nt, &no)) {
+        ncclResult_t r = rccl.Reduce(own, isroot ? recvbuf : NULL, (size_t) count, nt, no, root, c->nccl, s);
+        if (r != ncclSuccess) {
+            MPIR_Err_set_detail("ncclReduce: %s", rccl.GetErrorString ? rccl.GetErrorString(r) : "?");
+            rc = MPI_ERR_OTHER;
+        }
+        goto done_sync;
+    }
+
+    pof2 = pof2_of(p);
+    if (p == 1) {
+        if (sendbuf != MPI_IN_PLACE)
+            HIPTRY(hipMemcpyAsync(recvbuf, sendbuf, bytes, hipMemcpyDeviceToDevice, s));
+        goto done_sync;
+    }
+    if (bytes <= REDUCE_SHORT_MSG_SIZE || count < pof2) {
+        /* binomial: slot rel holds x_{(rel + root) % p}; the tree folds relranks */
+        int mask;
+        slot = (bytes + 255) & ~(size_t) 255;
+        if (!isroot) {
+            xfer_t x = { (void *) own, bytes, root };
+            TRY(group_exchange(c, &x, 1, NULL, 0, s));
+            goto done_sync;
+        }
+        if (comm_scratch(c, (size_t) p * slot, &scr)) {
+            MPIR_Err_set_detail("%s: scratch allocation failed", fc);
+            rc = MPI_ERR_NO_MEM;
+            goto done;
+        }
+        HIPTRY(hipMemcpyAsync(scr, own, bytes, hipMemcpyDeviceToDevice, s));
+        for (i = 1; i < p; i++) {
+            recvs[nrecv].buf = scr + (size_t) i * slot;
+            recvs[nrecv].bytes = bytes;
+            recvs[nrecv++].peer = (i + root) % p;
+        }
+        TRY(group_exchange(c, NULL, 0, recvs, nrecv, s));
+        if ((p & (p - 1)) == 0) {
+            const void *ys[64];
+            for (i = 0; i < p; i++)
+                ys[i] = scr + (size_t) i * slot;
+            TRY(fold_tree(ys, p, recvbuf, count, opidx, elem, s, fc));
+            goto done_sync;
+        }
+        for (mask = 1; mask < p; mask <<= 1)
+            for (i = 0; i + mask < p; i += 2 * mask)
+                TRY(fold_step(scr + (size_t) (i + mask) * slot, scr + (size_t) i * slot, count, opidx, elem, s, fc));
+        HIPTRY(hipMemcpyAsync(recvbuf, scr, bytes, hipMemcpyDeviceToDevice, s));
+        goto done_sync;
+    }
+
+    /* long: reduce-scatter on `work` (recvbuf at the root, scratch elsewhere) */
+    rem = p - pof2;
+    bits = 0;
+    while ((1 << bits) < pof2)
+        bits++;
+    cnts_disps(count, pof2, cnts, disps);
+    slot = ((size_t) (pof2 - 1) * (size_t) cnts[0] * esz + bytes + 256 + 255) & ~(size_t) 255;
+    if (comm_scratch(c, slot + (isroot ? 0 : bytes), &scr)) {
+        MPIR_Err_set_detail("%s: scratch allocation failed", fc);
+        rc = MPI_ERR_NO_MEM;
+        goto done;
+    }
+    work = isroot ? (char *) recvbuf : scr + slot;
+    if (work != own)
+        HIPTRY(hipMemcpyAsync(work, own, bytes, hipMemcpyDeviceToDevice, s));
+    TRY(rsg_phase(c, work, count, esz, opidx, elem, s, fc, scr, cnts, disps, &newrank));
+
+    /* gather of the owners' blocks to the root (reduce_intra_reduce_scatter_gather.c:256-410) */
+    if (newrank >= 0 && !isroot) {
+        int mb = bitrev(newrank, bits);
+        sends[nsend].buf = work + disps[mb] * esz;
+        sends[nsend].bytes = (size_t) cnts[mb] * esz;
+        sends[nsend++].peer = root;
+    }
+    if (isroot) {
+        for (i = 0; i < pof2; i++) {
+            int real = i < rem ? 2 * i : i + rem, b = bitrev(i, bits);
+            if (real == c->rank)
+                continue;
+            recvs[nrecv].buf = (char *) recvbuf + disps[b] * esz;
+            recvs[nrecv].bytes = (size_t) cnts[b] * esz;
+            recvs[nrecv++].peer = real;
+        }
+    }
+    TRY(group_exchange(c, sends, nsend, recvs, nrecv, s));
 
   done_sync:
     if (rc == MPI_SUCCESS && !hip_stream)

@@ -94,6 +94,10 @@ static const char *class_string(int cls)
         return "Invalid count";
     case MPI_ERR_TYPE:
         return "Invalid datatype";
+    case 5:     /* MPI_ERR_COMM */
+        return "Invalid communicator";
+    case 7:     /* MPI_ERR_ROOT */
+        return "Invalid root";
     case MPI_ERR_OP:
         return "Invalid MPI_Op";
     case MPI_ERR_ARG:

@@ -13,11 +13,14 @@
 #define PIP_MAX_RANKS   64
 #define PIP_CHUNK       ((size_t) 1 << 20)
 
+/* `owner` is the whole hand-over state in ONE word: 0 = the data area is free,
+ * dst + 1 = it holds a chunk for rank dst.  A receiver matches its own rank and
+ * acquires the chunk with a single load; a separate (full, dst) pair could be
+ * read across a recycle of the slot for another destination and lose a chunk. */
 typedef struct {
-    _Atomic uint32_t full;      /* 1: data area holds a chunk for `dst` */
-    int32_t dst;
+    _Atomic uint32_t owner;
     uint32_t bytes;
-    char pad[52];
+    char pad[56];
 } pip_slot_t;
 
 typedef struct {

@@ -5,8 +5,8 @@
  * Ranks are the processes bin/mpiexec forks; they attach the POSIX shm
  * segment named by MPIR_PIP_SHM.  Each rank owns one mailbox slot plus a
  * PIP_CHUNK-byte data area in that segment; a message is a sequence of
- * chunks, each handed over with a release-store of the slot's `full` flag
- * and returned with a release-store of 0 by the receiver.  Because every rank
+ * chunks, each handed over with a release-store of dst + 1 into the slot's
+ * `owner` word and returned with a release-store of 0 by the receiver.  Because every rank
  * issues the same collectives in the same order and pairs exchange FIFO, no
  * tags are needed.  A rank started without mpiexec is a singleton (size 1).
  *
@@ -75,26 +75,25 @@ static void sendrecv(const void *sbuf, size_t sbytes, int dst, void *rbuf, size_
     int sdone = dst < 0, rdone = src < 0, sfirst = 1, rfirst = 1;
     while (!sdone || !rdone) {
         int moved = 0;
-        if (!sdone && atomic_load_explicit(&mine->full, memory_order_acquire) == 0) {
+        if (!sdone && atomic_load_explicit(&mine->owner, memory_order_acquire) == 0) {
             size_t n = sbytes - soff < PIP_CHUNK ? sbytes - soff : PIP_CHUNK;
             if (n)
                 memcpy(slot_data(W.rank), (const char *) sbuf + soff, n);
-            mine->dst = dst;
             mine->bytes = (uint32_t) n;
-            atomic_store_explicit(&mine->full, 1, memory_order_release);
+            atomic_store_explicit(&mine->owner, (uint32_t) dst + 1, memory_order_release);
             soff += n;
             sfirst = 0;
             sdone = soff >= sbytes && !sfirst;
             moved = 1;
         }
-        if (!rdone && atomic_load_explicit(&theirs->full, memory_order_acquire) == 1 && theirs->dst == W.rank) {
+        if (!rdone && atomic_load_explicit(&theirs->owner, memory_order_acquire) == (uint32_t) W.rank + 1) {
             size_t n = theirs->bytes;
             if (roff + n > rbytes)      /* truncation: the message is longer than the receive buffer */
                 n = rbytes - roff;
             if (n)
                 memcpy((char *) rbuf + roff, slot_data(src), n);
             roff += theirs->bytes;
-            atomic_store_explicit(&theirs->full, 0, memory_order_release);
+            atomic_store_explicit(&theirs->owner, 0, memory_order_release);
             rfirst = 0;
             rdone = roff >= rbytes && !rfirst;
             moved = 1;
@@ -104,7 +103,7 @@ static void sendrecv(const void *sbuf, size_t sbytes, int dst, void *rbuf, size_
     }
     /* the last outgoing chunk must be consumed before the buffer is reused */
     if (dst >= 0)
-        while (atomic_load_explicit(&mine->full, memory_order_acquire) != 0)
+        while (atomic_load_explicit(&mine->owner, memory_order_acquire) != 0)
             relax();
 }
 

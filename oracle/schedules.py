@@ -291,3 +291,16 @@ def reduce_scatter_block_auto(rank_sendbufs: list[np.ndarray], recvcount: int, e
     if len(rank_sendbufs) * recvcount * esz < RSB_COMMUTATIVE_LONG_MSG_SIZE:
         return reduce_scatter_block_recursive_halving(rank_sendbufs, recvcount, esz, dt, op)
     return reduce_scatter_block_pairwise(rank_sendbufs, recvcount, esz, dt, op)
+
+
+def reduce_auto(rank_bufs: list[np.ndarray], count: int, esz: int, dt: int, op: int, root: int) -> np.ndarray:
+    """MPI_Reduce's result at `root` on one node: reduce_intra_smp.c runs
+    MPIR_Reduce_intra_auto over node_comm with the real root (reduce.c:214):
+    binomial tree rooted at `root` for short messages, else
+    reduce_scatter_gather, whose block values do not depend on the root."""
+    p = len(rank_bufs)
+    if p == 1:
+        return rank_bufs[0].view(np.uint8).reshape(-1).copy()
+    if count * esz > REDUCE_SHORT_MSG_SIZE and count >= _pof2(p):
+        return allreduce_smp(rank_bufs, count, esz, dt, op)
+    return reduce_binomial(rank_bufs, count, esz, dt, op, root=root)

@@ -162,6 +162,76 @@ def test_algorithm_switch_points(mpi, orc, cuda, t, op, p):
             mpi.comm_free(c)
 
 
+RCASES = [("MPI_FLOAT", "MPI_SUM"), ("MPIX_C_FLOAT16", "MPI_SUM"), ("MPI_DOUBLE", "MPI_MAX"),
+          ("MPI_INT64_T", "MPI_PROD"), ("MPI_DOUBLE_INT", "MPI_MINLOC")]
+
+
+@pytest.mark.parametrize("t,op", RCASES, ids=[f"{t}-{o}" for t, o in RCASES])
+@pytest.mark.parametrize("p", [1, 2, 3, 5, 8])
+@pytest.mark.parametrize("inplace", [False, True])
+def test_reduce_reference_order(mpi, orc, cuda, t, op, p, inplace):
+    """MPIX_Reduce_hip at every root: binomial (short) and reduce-scatter + gather
+    (long) vs the step-by-step schedules; non-root recvbufs are NULL and the
+    root's recvbuf is the only buffer written."""
+    from oracle import schedules as S
+    torch = cuda
+    esz = T.elem_size(t)
+    dt, o = mpi.DATATYPES[t], mpi.OPS[op]
+    comms = mpi.comm_create_loopback(p)
+    try:
+        for count, seed in ((3, 7 * p), (2048 // esz, p), ((1 << 16) + 5, 3 * p)):
+            rng = np.random.default_rng(seed)
+            xs = [T.to_bytes(T.gen(t, count, rng, op)) for _ in range(p)]
+            send = [torch.from_numpy(x.copy()).cuda() for x in xs]
+            for root in range(p):
+                want = S.reduce_auto(xs, count, esz, dt, o, root)
+                rbuf = send[root].clone() if inplace else torch.zeros_like(send[root])
+                keep = [s.clone() for s in send]
+                torch.cuda.synchronize()
+
+                def rank(r):
+                    sb = mpi.MPI_IN_PLACE if (inplace and r == root) else send[r].data_ptr()
+                    rb = rbuf.data_ptr() if r == root else 0
+                    _ok(mpi, mpi.reduce(sb, rb, count, dt, o, root, comms[r], mpi.MPIX_HIP_ALG_REFERENCE_ORDER))
+
+                run_ranks(rank, p)
+                torch.cuda.synchronize()
+                got = rbuf.cpu().numpy()
+                bad = np.nonzero((got != want).reshape(-1, esz).any(axis=1))[0][:4]
+                assert same(got, want, t), f"count {count} root {root}: elements {bad} got " \
+                    f"{[bytes(got[i * esz:(i + 1) * esz]).hex() for i in bad]} want " \
+                    f"{[bytes(want[i * esz:(i + 1) * esz]).hex() for i in bad]}"
+                for r in range(p):      # sendbufs are read-only
+                    assert torch.equal(send[r], keep[r]), f"rank {r} sendbuf modified"
+    finally:
+        for c in comms:
+            mpi.comm_free(c)
+
+
+def test_reduce_validation(mpi, cuda):
+    torch = cuda
+    comms = mpi.comm_create_loopback(2)
+    try:
+        a = torch.ones(4, device="cuda")
+        b = torch.zeros(4, device="cuda")
+        REF = mpi.MPIX_HIP_ALG_REFERENCE_ORDER
+        # invalid root -> MPI_ERR_ROOT (class 7)
+        assert mpi.reduce(a.data_ptr(), b.data_ptr(), 4, mpi.MPI_FLOAT, mpi.MPI_SUM, 2, comms[0], REF) & 0x7f == 7
+        assert mpi.reduce(a.data_ptr(), b.data_ptr(), 4, mpi.MPI_FLOAT, mpi.MPI_SUM, -1, comms[0], REF) & 0x7f == 7
+        # MPI_IN_PLACE at a non-root -> MPI_ERR_BUFFER
+        assert mpi.reduce(mpi.MPI_IN_PLACE, 0, 4, mpi.MPI_FLOAT, mpi.MPI_SUM, 0, comms[1], REF) & 0x7f == 1
+        # aliased buffers at the root -> MPI_ERR_BUFFER
+        assert mpi.reduce(a.data_ptr(), a.data_ptr(), 4, mpi.MPI_FLOAT, mpi.MPI_SUM, 0, comms[0], REF) & 0x7f == 1
+        # MPI_REPLACE is not a reduction op
+        assert mpi.reduce(a.data_ptr(), b.data_ptr(), 4, mpi.MPI_FLOAT, mpi.MPI_REPLACE, 0, comms[0], REF) \
+            & 0x7f == 9
+        # count 0 is a no-op
+        assert mpi.reduce(a.data_ptr(), b.data_ptr(), 0, mpi.MPI_FLOAT, mpi.MPI_SUM, 0, comms[0], REF) == 0
+    finally:
+        for c in comms:
+            mpi.comm_free(c)
+
+
 def _ok(mpi, rc):
     assert rc == 0, mpi.error_string(rc)
 

@@ -36,13 +36,20 @@ def _rank_main(rank, size, uid, q, cases):
         q.put((rank, "create", rc, mpi.error_string(rc)))
         return
     out = []
-    for t, op, count, alg in cases:
+    for kind, t, op, count, alg in cases:
         rng = np.random.default_rng(1000 + rank)
         x = T.to_bytes(T.gen(t, count, rng, op, specials=False))
         send = torch.from_numpy(x.copy()).cuda()
         recv = torch.zeros_like(send)
         torch.cuda.synchronize()
-        rc = mpi.allreduce(send.data_ptr(), recv.data_ptr(), count, mpi.DATATYPES[t], mpi.OPS[op], comm.value, alg)
+        if kind == "allreduce":
+            rc = mpi.allreduce(send.data_ptr(), recv.data_ptr(), count, mpi.DATATYPES[t], mpi.OPS[op], comm.value,
+                               alg)
+        else:   # reduce to the last rank; recvbuf NULL elsewhere
+            root = size - 1
+            rc = mpi.reduce(send.data_ptr(), recv.data_ptr() if rank == root else 0, count, mpi.DATATYPES[t],
+                            mpi.OPS[op], root, comm.value, alg)
+        torch.cuda.synchronize()
         out.append((rc, x, recv.cpu().numpy()))
     q.put((rank, "ok", 0, out))
     mpi.comm_free(comm.value)
@@ -75,24 +82,36 @@ def _ngpus():
 
 
 @pytest.mark.parametrize("size", [1, 2, 4, 8])
-def test_allreduce_over_rccl(mpi, orc, cuda, size):
+def test_allreduce_and_reduce_over_rccl(mpi, orc, cuda, size):
     from oracle import schedules as S
     if _ngpus() < size:
         pytest.skip(f"needs {size} GPUs, {_ngpus()} visible")
-    cases = [("MPI_FLOAT", "MPI_SUM", (1 << 20) + 3, mpi.MPIX_HIP_ALG_REFERENCE_ORDER),
-             ("MPI_FLOAT", "MPI_SUM", (1 << 20) + 3, mpi.MPIX_HIP_ALG_RCCL),
-             ("MPI_INT", "MPI_SUM", 4099, mpi.MPIX_HIP_ALG_RCCL),
-             ("MPIX_C_FLOAT16", "MPI_SUM", 4099, mpi.MPIX_HIP_ALG_REFERENCE_ORDER)]
+    REF, RCCL = mpi.MPIX_HIP_ALG_REFERENCE_ORDER, mpi.MPIX_HIP_ALG_RCCL
+    cases = [("allreduce", "MPI_FLOAT", "MPI_SUM", (1 << 20) + 3, REF),
+             ("allreduce", "MPI_FLOAT", "MPI_SUM", (1 << 20) + 3, RCCL),
+             ("allreduce", "MPI_INT", "MPI_SUM", 4099, RCCL),
+             ("allreduce", "MPIX_C_FLOAT16", "MPI_SUM", 4099, REF),
+             ("allreduce", "MPI_DOUBLE", "MPI_MAX", 100, REF),
+             ("reduce", "MPI_FLOAT", "MPI_SUM", (1 << 20) + 3, REF),
+             ("reduce", "MPI_FLOAT", "MPI_SUM", (1 << 20) + 3, RCCL),
+             ("reduce", "MPI_INT", "MPI_SUM", 77, RCCL),
+             ("reduce", "MPI_DOUBLE", "MPI_SUM", 77, REF)]
     res = _run(size, cases)
     for r in range(size):
         assert res[r][1] == "ok", res[r]
-    for k, (t, op, count, alg) in enumerate(cases):
+    for k, (kind, t, op, count, alg) in enumerate(cases):
         xs = [res[r][3][k][1] for r in range(size)]
         esz = T.elem_size(t)
-        want = S.allreduce_smp_auto(xs, count, esz, mpi.DATATYPES[t], mpi.OPS[op]) if size > 1 else xs[0]
+        if kind == "allreduce":
+            want = S.allreduce_smp_auto(xs, count, esz, mpi.DATATYPES[t], mpi.OPS[op]) if size > 1 else xs[0]
+            checked = range(size)
+        else:
+            want = S.reduce_auto(xs, count, esz, mpi.DATATYPES[t], mpi.OPS[op], size - 1)
+            checked = [size - 1]
         for r in range(size):
+            assert res[r][3][k][0] == 0, (kind, t, alg, r)
+        for r in checked:
             rc, _, got = res[r][3][k]
-            assert rc == 0
             if alg == mpi.MPIX_HIP_ALG_REFERENCE_ORDER or t == "MPI_INT":
                 assert np.array_equal(got, want), (t, alg, r)
             else:

@@ -125,3 +125,43 @@ def test_multi_validation(mpi, cuda):
     h = np.zeros(64, np.float32)
     assert mpi.reduce_local_multi([h.ctypes.data, a.data_ptr()], b.data_ptr(), 64, mpi.MPI_FLOAT, mpi.MPI_SUM,
                                   mpi.MPIX_ORDER_CHAIN) == mpi.MPI_ERR_BUFFER
+
+
+ANY = [("MPI_DOUBLE_INT", "MPI_MINLOC"), ("MPI_2INT", "MPI_MAXLOC"), ("MPI_INT", "MPI_LAND"),
+       ("MPI_UNSIGNED_SHORT", "MPI_BOR"), ("MPI_C_DOUBLE_COMPLEX", "MPI_PROD"), ("MPI_LONG_DOUBLE", "MPI_SUM"),
+       ("MPI_LONG_DOUBLE_INT", "MPI_MAXLOC"), ("MPI_FLOAT", "MPI_SUM"), ("MPIX_C_FLOAT16", "MPI_MAX")]
+
+
+@pytest.mark.parametrize("t,op", ANY, ids=[f"{t}-{o}" for t, o in ANY])
+@pytest.mark.parametrize("n,order", [(2, "TREE"), (4, "TREE"), (16, "TREE"), (64, "TREE"), (3, "CHAIN"),
+                                     (13, "CHAIN")])
+def test_one_pass_combine_matches_stepwise_fold(mpi, orc, cuda, t, op, n, order):
+    """MPIR_Hip_combine's general one-pass path (k_combine_any: any op/type, any n,
+    no device temporaries) and the fused kernels agree bit for bit with the
+    same fold done one MPIR_Reduce_local step at a time by the oracle.  The
+    output aliases operand 0 on the CHAIN cases."""
+    torch = cuda
+    esz = T.elem_size(t)
+    count = 1000 + n
+    rng = np.random.default_rng(n)
+    xs = [T.to_bytes(T.gen(t, count, rng, op)) for _ in range(n)]
+    dt, o = mpi.DATATYPES[t], mpi.OPS[op]
+    acc = [x.copy() for x in xs]
+    if order == "TREE":
+        step = 1
+        while step < n:
+            for j in range(0, n, 2 * step):
+                assert orc.reduce_local(acc[j + step], acc[j], count, dt, o, check=False) == 0
+            step *= 2
+    else:
+        for j in range(1, n):
+            assert orc.reduce_local(acc[j], acc[0], count, dt, o, check=False) == 0
+    want = acc[0]
+    dev = [torch.from_numpy(x.copy()).cuda() for x in xs]
+    out = dev[0] if order == "CHAIN" else torch.zeros(count * esz, dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
+    rc = mpi.reduce_local_multi([d.data_ptr() for d in dev], out.data_ptr(), count, dt, o,
+                                mpi.MPIX_ORDER_TREE if order == "TREE" else mpi.MPIX_ORDER_CHAIN)
+    assert rc == 0, mpi.error_string(rc)
+    torch.cuda.synchronize()
+    assert same(out.cpu().numpy(), want, t)

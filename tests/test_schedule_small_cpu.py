@@ -130,3 +130,20 @@ def test_algorithm_switch_points(orc):
         fn = S.reduce_scatter_block_recursive_halving if small else S.reduce_scatter_block_pairwise
         ref = fn(xs, rc, 4, DATATYPES["MPI_FLOAT"], OPS["MPI_SUM"])
         assert all(np.array_equal(a, b) for a, b in zip(got, ref))
+
+
+@pytest.mark.parametrize("t,op", CASES)
+@pytest.mark.parametrize("p", [2, 3, 5, 6, 8])
+def test_reduce_short_binomial_plan_any_root(orc, t, op, p):
+    """MPI_Reduce, short messages: the binomial tree rooted at `root`
+    (relrank = rank - root) is the binomial fold over slots in relrank order."""
+    from oracle import schedules as S
+    esz = T.elem_size(t)
+    count = 5
+    xs = _inputs(t, op, count, p, 31 * p)
+    for root in range(p):
+        want = S.reduce_auto(xs, count, esz, DATATYPES[t], OPS[op], root)
+        slots = [xs[(rel + root) % p].copy() for rel in range(p)]
+        for dst, src in binomial_plan(p):
+            _red(orc, slots[src], slots[dst], count, t, op)
+        assert np.array_equal(slots[0], want), f"root {root}"
