@@ -60,7 +60,7 @@ int MPIX_Hip_comm_size(MPIX_Hip_comm comm, int *size);
 /* MPI_Allreduce semantics (sendbuf may be MPI_IN_PLACE). */
 int MPIX_Allreduce_hip(const void *sendbuf, void *recvbuf, int count, MPI_Datatype datatype, MPI_Op op,
                        MPIX_Hip_comm comm, int algorithm, void *hip_stream);
-/* MPI_Reduce semantics (reduce.c:742; MPI_IN_PLACE at the root only; recvbuf
+/* MPI_Reduce semantics (reduce.c:382; MPI_IN_PLACE at the root only; recvbuf
  * significant at the root only).  Reference order: reduce_intra_smp.c ->
  * MPIR_Reduce_intra_auto on the node (binomial tree rooted at `root` for
  * count*size <= 2048 or count < pof2, else reduce-scatter + gather);
@@ -70,6 +70,13 @@ int MPIX_Reduce_hip(const void *sendbuf, void *recvbuf, int count, MPI_Datatype 
 /* MPI_Reduce_scatter_block semantics (sendbuf may be MPI_IN_PLACE). */
 int MPIX_Reduce_scatter_block_hip(const void *sendbuf, void *recvbuf, int recvcount, MPI_Datatype datatype,
                                   MPI_Op op, MPIX_Hip_comm comm, int algorithm, void *hip_stream);
+/* MPI_Reduce_scatter semantics (reduce_scatter.c:383; rank q receives
+ * recvcounts[q] elements; sendbuf may be MPI_IN_PLACE).  Reference order:
+ * MPIR_Reduce_scatter_intra_auto (recursive halving below 524288 total bytes,
+ * else pairwise); MPIX_HIP_ALG_RCCL: ncclReduceScatter when the counts are
+ * all equal, else the reference order. */
+int MPIX_Reduce_scatter_hip(const void *sendbuf, void *recvbuf, const int recvcounts[], MPI_Datatype datatype,
+                            MPI_Op op, MPIX_Hip_comm comm, int algorithm, void *hip_stream);
 
 #ifdef __cplusplus
 }

@@ -453,38 +453,43 @@ static int allreduce_short(struct MPIX_Hip_comm_s *c, const void *sendbuf, void 
     return e == hipSuccess ? MPI_SUCCESS : hip_err(fc, e);
 }
 
-/* MPI_Reduce_scatter_block, p*recvcount*size < 524288: recursive halving
- * (reduce_scatter_block_intra_recursive_halving.c).  Block r is finished by
- * newrank n = r/2 (r < 2*rem) or r - rem, as
+/* MPI_Reduce_scatter(_block), total bytes < 524288: recursive halving
+ * (reduce_scatter_block_intra_recursive_halving.c; reduce_scatter_intra_
+ * recursive_halving.c is the same schedule with per-rank counts).  Block r is
+ * finished by newrank n = r/2 (r < 2*rem) or r - rem, as
  *   Y_m = x_{2m+1} (+) x_{2m} for m < rem (pre-fold :163-195), else x_{m+rem};
  *   tree ((z0+z1)+(z2+z3))+... over z_k = Y_{n ^ bitrev(k)} (halving :197-283,
  *   mask = pof2/2 first, received data second).
  * Here: one all-to-all of blocks (every rank gets x_q's block r from each q),
- * the rem pre-fold steps, one fused tree combine into recvbuf. */
-static int reduce_scatter_block_short(struct MPIX_Hip_comm_s *c, const char *src, void *recvbuf, long recvcount,
-                                      size_t esz, int opidx, int elem, hipStream_t s, const char *fc)
+ * the rem pre-fold steps, one tree combine into recvbuf. */
+static int reduce_scatter_short(struct MPIX_Hip_comm_s *c, const char *src, void *recvbuf, const long *cnts,
+                                const long *disps, size_t esz, int opidx, int elem, hipStream_t s, const char *fc)
 {
     int p = c->size, q, nx = 0, rc = MPI_SUCCESS, pof2 = pof2_of(p), rem = p - pof2, bits = 0, n, k, m;
-    size_t nb = (size_t) recvcount * esz, slot = (nb + 255) & ~(size_t) 255;
+    long rcount = cnts[c->rank];
+    size_t nb = (size_t) rcount * esz, slot = (nb + 255) & ~(size_t) 255;
     xfer_t sends[MAX_XFER], recvs[MAX_XFER];
     const void *ys[64];
     char *scr = NULL;
     hipError_t e;
     while ((1 << bits) < pof2)
         bits++;
-    if (comm_scratch(c, (size_t) p * slot, &scr)) {
+    if (comm_scratch(c, (size_t) p * slot + 256, &scr)) {
         MPIR_Err_set_detail("%s: scratch allocation failed", fc);
         return MPI_ERR_NO_MEM;
     }
     /* own block into its slot: the pre-fold updates slots in place */
-    e = hipMemcpyAsync(scr + (size_t) c->rank * slot, src + (size_t) c->rank * nb, nb, hipMemcpyDeviceToDevice, s);
-    if (e != hipSuccess)
-        return hip_err(fc, e);
+    if (nb) {
+        e = hipMemcpyAsync(scr + (size_t) c->rank * slot, src + (size_t) disps[c->rank] * esz, nb,
+                           hipMemcpyDeviceToDevice, s);
+        if (e != hipSuccess)
+            return hip_err(fc, e);
+    }
     for (q = 0; q < p; q++) {
         if (q == c->rank)
             continue;
-        sends[nx].buf = (void *) (src + (size_t) q * nb);
-        sends[nx].bytes = nb;
+        sends[nx].buf = (void *) (src + (size_t) disps[q] * esz);
+        sends[nx].bytes = (size_t) cnts[q] * esz;
         sends[nx].peer = q;
         recvs[nx].buf = scr + (size_t) q * slot;
         recvs[nx].bytes = nb;
@@ -492,8 +497,10 @@ static int reduce_scatter_block_short(struct MPIX_Hip_comm_s *c, const char *src
     }
     if ((rc = group_exchange(c, sends, nx, recvs, nx, s)) != MPI_SUCCESS)
         return rc;
+    if (!rcount)
+        return MPI_SUCCESS;
     for (m = 0; m < rem; m++)
-        if ((rc = fold_step(scr + (size_t) (2 * m) * slot, scr + (size_t) (2 * m + 1) * slot, recvcount, opidx,
+        if ((rc = fold_step(scr + (size_t) (2 * m) * slot, scr + (size_t) (2 * m + 1) * slot, rcount, opidx,
                             elem, s, fc)) != MPI_SUCCESS)
             return rc;
     n = c->rank < 2 * rem ? c->rank / 2 : c->rank - rem;
@@ -501,7 +508,7 @@ static int reduce_scatter_block_short(struct MPIX_Hip_comm_s *c, const char *src
         int y = n ^ bitrev(k, bits);
         ys[k] = scr + (size_t) (y < rem ? 2 * y + 1 : y + rem) * slot;
     }
-    return fold_tree(ys, pof2, recvbuf, recvcount, opidx, elem, s, fc);
+    return fold_tree(ys, pof2, recvbuf, rcount, opidx, elem, s, fc);
 }
 
 /* validation shared by both collectives (MPIR_ERRTEST_OP + check_dtype) */
@@ -881,14 +888,22 @@ int MPIX_Reduce_hip(const void *sendbuf, void *recvbuf, int count, MPI_Datatype 
     return rc ? MPIR_Err_return(fc, rc) : MPI_SUCCESS;
 }
 
-/* ------------------------------------------------------------ Reduce_scatter_block */
-int MPIX_Reduce_scatter_block_hip(const void *sendbuf, void *recvbuf, int recvcount, MPI_Datatype datatype,
-                                  MPI_Op op, MPIX_Hip_comm comm, int algorithm, void *hip_stream)
+/* ------------------------------------------------------------ Reduce_scatter(_block)
+ * One implementation for both: counts[q] elements of the result go to rank q.
+ *   RCCL:  ncclReduceScatter (regular counts only).
+ *   reference order (MPIR_Reduce_scatter(_block)_intra_auto, builtin ops are
+ *   commutative): recursive halving below 524288 total bytes, else pairwise
+ *   (reduce_scatter_block_intra_pairwise.c:97-134 /
+ *   reduce_scatter_intra_pairwise.c): block r = ((x_r + x_{r-1}) + x_{r-2}) + ...
+ *   as one all-to-all + one CHAIN combine. */
+static int reduce_scatter_common(const char *fc, const void *sendbuf, void *recvbuf, const int *counts,
+                                 MPI_Datatype datatype, MPI_Op op, MPIX_Hip_comm comm, int algorithm,
+                                 void *hip_stream)
 {
-    static const char *fc = "MPIX_Reduce_scatter_block_hip";
     struct MPIX_Hip_comm_s *c = comm;
-    int elem = 0, opidx = op & 0xf, rc, p, i, cur = 0;
-    size_t esz, nb;
+    int elem = 0, opidx = op & 0xf, rc, p, i, cur = 0, regular = 1;
+    long cnts[64] = {0}, disps[64] = {0}, total = 0;
+    size_t esz, nb, slot;
     hipStream_t s;
     ncclDataType_t nt;
     ncclRedOp_t no;
@@ -897,24 +912,39 @@ int MPIX_Reduce_scatter_block_hip(const void *sendbuf, void *recvbuf, int recvco
     const char *src;
     char *scr = NULL;
 
-    rc = coll_check(fc, sendbuf, recvbuf, recvcount, datatype, op, comm, &elem);
+    if (!comm) {
+        MPIR_Err_set_detail("%s: null communicator", fc);
+        return MPIR_Err_return(fc, MPI_ERR_ARG);
+    }
+    p = c->size;
+    for (i = 0; i < p; i++) {
+        if (counts[i] < 0) {
+            MPIR_Err_set_detail("%s: negative count", fc);
+            return MPIR_Err_return(fc, MPI_ERR_COUNT);
+        }
+        cnts[i] = counts[i];
+        disps[i] = total;
+        total += counts[i];
+        regular &= counts[i] == counts[0];
+    }
+    /* op / type validation; the alias check applies when any data moves */
+    rc = coll_check(fc, sendbuf, recvbuf, total > 0, datatype, op, comm, &elem);
     if (rc)
         return MPIR_Err_return(fc, rc);
-    if (recvcount == 0)
+    if (total == 0)
         return MPI_SUCCESS;
     if (hipGetDevice(&cur) == hipSuccess && cur != c->device)
         (void) hipSetDevice(c->device);
     s = hip_stream ? (hipStream_t) hip_stream : c->stream;
     esz = MPIR_Hip_elem_size(elem);
-    nb = (size_t) recvcount * esz;
-    p = c->size;
+    nb = (size_t) cnts[c->rank] * esz;
     src = sendbuf == MPI_IN_PLACE ? (const char *) recvbuf : (const char *) sendbuf;
 
-    if (want_rccl(c, algorithm, elem, opidx, &nt, &no)) {
+    if (regular && want_rccl(c, algorithm, elem, opidx, &nt, &no)) {
         ncclResult_t r;
         /* NCCL's in-place form is recvbuff == sendbuff + rank * recvcount */
         void *dst = sendbuf == MPI_IN_PLACE ? (char *) recvbuf + (size_t) c->rank * nb : recvbuf;
-        r = rccl.ReduceScatter(src, dst, (size_t) recvcount, nt, no, c->nccl, s);
+        r = rccl.ReduceScatter(src, dst, (size_t) cnts[0], nt, no, c->nccl, s);
         if (r != ncclSuccess) {
             MPIR_Err_set_detail("ncclReduceScatter: %s", rccl.GetErrorString ? rccl.GetErrorString(r) : "?");
             rc = MPI_ERR_OTHER;
@@ -925,38 +955,42 @@ int MPIX_Reduce_scatter_block_hip(const void *sendbuf, void *recvbuf, int recvco
         goto done_sync;
     }
 
-    /* ---- reference order: MPIR_Reduce_scatter_block_intra_auto (reduce_scatter_block.c:136-148)
-     * takes recursive halving below 524288 total bytes for commutative (all builtin) ops */
-    if (p > 1 && (size_t) p * nb < RSB_COMMUTATIVE_LONG_MSG_SIZE) {
-        TRY(reduce_scatter_block_short(c, src, recvbuf, recvcount, esz, opidx, elem, s, fc));
+    if (p > 1 && (size_t) total * esz < RSB_COMMUTATIVE_LONG_MSG_SIZE) {
+        TRY(reduce_scatter_short(c, src, recvbuf, cnts, disps, esz, opidx, elem, s, fc));
         goto done_sync;
     }
-    /* long: pairwise (reduce_scatter_block_intra_pairwise.c:97-134):
-     * block r = ((x_r + x_{r-1}) + x_{r-2}) + ...; y_i = block r from rank r - i */
-    if (comm_scratch(c, (size_t) (p > 1 ? p - 1 : 1) * nb + 256, &scr)) {
+    /* long: pairwise.  y_i = block r from rank r - i into scratch slot i-1; in
+     * place, the own block is staged too when it overlaps the output. */
+    slot = (nb + 255) & ~(size_t) 255;
+    if (comm_scratch(c, (size_t) p * slot + 256, &scr)) {
         MPIR_Err_set_detail("%s: scratch allocation failed", fc);
         rc = MPI_ERR_NO_MEM;
         goto done;
     }
+    ys[0] = src + (size_t) disps[c->rank] * esz;
+    if (sendbuf == MPI_IN_PLACE && disps[c->rank] > 0 && disps[c->rank] < cnts[c->rank]) {
+        HIPTRY(hipMemcpyAsync(scr + (size_t) (p - 1) * slot, ys[0], nb, hipMemcpyDeviceToDevice, s));
+        ys[0] = scr + (size_t) (p - 1) * slot;
+    }
     for (i = 1; i < p; i++) {
         int dst = (c->rank + i) % p, from = (c->rank - i + p) % p;
-        sends[i - 1].buf = (void *) (src + (size_t) dst * nb);
-        sends[i - 1].bytes = nb;
+        sends[i - 1].buf = (void *) (src + (size_t) disps[dst] * esz);
+        sends[i - 1].bytes = (size_t) cnts[dst] * esz;
         sends[i - 1].peer = dst;
-        recvs[i - 1].buf = scr + (size_t) (i - 1) * nb;
+        recvs[i - 1].buf = scr + (size_t) (i - 1) * slot;
         recvs[i - 1].bytes = nb;
         recvs[i - 1].peer = from;
+        ys[i] = scr + (size_t) (i - 1) * slot;
     }
     if (p > 1)
         TRY(group_exchange(c, sends, p - 1, recvs, p - 1, s));
-    ys[0] = src + (size_t) c->rank * nb;
-    for (i = 1; i < p; i++)
-        ys[i] = scr + (size_t) (i - 1) * nb;
-    rc = MPIR_Hip_combine(ys, p, recvbuf, (uint64_t) recvcount, opidx, elem, MPIR_HIP_ORDER_CHAIN, s, 0);
-    if (rc) {
-        MPIR_Op_report_hip_error(fc, rc);
-        rc = MPI_ERR_OTHER;
-        goto done;
+    if (nb) {
+        rc = MPIR_Hip_combine(ys, p, recvbuf, (uint64_t) cnts[c->rank], opidx, elem, MPIR_HIP_ORDER_CHAIN, s, 0);
+        if (rc) {
+            MPIR_Op_report_hip_error(fc, rc);
+            rc = MPI_ERR_OTHER;
+            goto done;
+        }
     }
 
   done_sync:
@@ -966,4 +1000,28 @@ int MPIX_Reduce_scatter_block_hip(const void *sendbuf, void *recvbuf, int recvco
     if (cur != c->device)
         (void) hipSetDevice(cur);
     return rc ? MPIR_Err_return(fc, rc) : MPI_SUCCESS;
+}
+
+int MPIX_Reduce_scatter_block_hip(const void *sendbuf, void *recvbuf, int recvcount, MPI_Datatype datatype,
+                                  MPI_Op op, MPIX_Hip_comm comm, int algorithm, void *hip_stream)
+{
+    int counts[64], i;
+    if (!comm || recvcount < 0)
+        return reduce_scatter_common("MPIX_Reduce_scatter_block_hip", sendbuf, recvbuf,
+                                     (int[64]) { recvcount }, datatype, op, comm, algorithm, hip_stream);
+    for (i = 0; i < comm->size; i++)
+        counts[i] = recvcount;
+    return reduce_scatter_common("MPIX_Reduce_scatter_block_hip", sendbuf, recvbuf, counts, datatype, op, comm,
+                                 algorithm, hip_stream);
+}
+
+int MPIX_Reduce_scatter_hip(const void *sendbuf, void *recvbuf, const int recvcounts[], MPI_Datatype datatype,
+                            MPI_Op op, MPIX_Hip_comm comm, int algorithm, void *hip_stream)
+{
+    if (!recvcounts) {
+        MPIR_Err_set_detail("MPIX_Reduce_scatter_hip: recvcounts is NULL");
+        return MPIR_Err_return("MPIX_Reduce_scatter_hip", MPI_ERR_ARG);
+    }
+    return reduce_scatter_common("MPIX_Reduce_scatter_hip", sendbuf, recvbuf, recvcounts, datatype, op, comm,
+                                 algorithm, hip_stream);
 }

@@ -114,7 +114,7 @@ EXPORTED_SYMBOLS = [
     # device collectives (include/mpix_hip_coll.h)
     "MPIX_Hip_comm_get_unique_id", "MPIX_Hip_comm_create", "MPIX_Hip_comm_create_loopback",
     "MPIX_Hip_comm_free", "MPIX_Hip_comm_rank", "MPIX_Hip_comm_size",
-    "MPIX_Allreduce_hip", "MPIX_Reduce_scatter_block_hip", "MPIX_Reduce_hip",
+    "MPIX_Allreduce_hip", "MPIX_Reduce_scatter_block_hip", "MPIX_Reduce_hip", "MPIX_Reduce_scatter_hip",
     # the HIP shim (include/mpir_hip_reduce.h)
     "MPIR_Hip_reduce", "MPIR_Hip_elem_size", "MPIR_Hip_has_kernel", "MPIR_Hip_is_device_ptr",
     "MPIR_Hip_memcpy", "MPIR_Hip_error_string", "MPIR_Hip_device_count",
@@ -163,6 +163,8 @@ def load(path: str | None = None) -> ctypes.CDLL:
         f.restype = i32
     lib.MPIX_Reduce_hip.argtypes = [vp, vp, i32, i32, i32, i32, vp, i32, vp]
     lib.MPIX_Reduce_hip.restype = i32
+    lib.MPIX_Reduce_scatter_hip.argtypes = [vp, vp, ctypes.POINTER(i32), i32, i32, vp, i32, vp]
+    lib.MPIX_Reduce_scatter_hip.restype = i32
     lib.MPIX_Reduce_local_set_errhandler.argtypes = [i32]
     lib.MPIX_Reduce_local_set_errhandler.restype = i32
     lib.MPI_Op_create.argtypes = [MPI_User_function, i32, ctypes.POINTER(i32)]
@@ -248,6 +250,14 @@ def reduce(sendbuf, recvbuf, count: int, datatype: int, op: int, root: int, comm
     """MPIX_Reduce_hip (recvbuf significant at the root only; may be 0 elsewhere)."""
     return load().MPIX_Reduce_hip(ctypes.c_void_p(sendbuf), ctypes.c_void_p(recvbuf), count, datatype, op, root,
                                   ctypes.c_void_p(comm), algorithm, ctypes.c_void_p(stream or None))
+
+
+def reduce_scatter(sendbuf, recvbuf: int, recvcounts, datatype: int, op: int, comm, algorithm: int = 0,
+                   stream: int = 0) -> int:
+    """MPIX_Reduce_scatter_hip (per-rank recvcounts)."""
+    arr = (ctypes.c_int * len(recvcounts))(*recvcounts)
+    return load().MPIX_Reduce_scatter_hip(ctypes.c_void_p(sendbuf), ctypes.c_void_p(recvbuf), arr, datatype, op,
+                                          ctypes.c_void_p(comm), algorithm, ctypes.c_void_p(stream or None))
 
 
 def reduce_scatter_block(sendbuf, recvbuf: int, recvcount: int, datatype: int, op: int, comm,

@@ -211,21 +211,24 @@ def allreduce_smp_auto(rank_bufs: list[np.ndarray], count: int, esz: int, dt: in
     return reduce_binomial(rank_bufs, count, esz, dt, op, root=0)
 
 
-def reduce_scatter_block_recursive_halving(rank_sendbufs: list[np.ndarray], recvcount: int, esz: int,
-                                           dt: int, op: int) -> list[np.ndarray]:
-    """Each rank's recvbuf after MPI_Reduce_scatter_block's recursive halving
-    (reduce_scatter_block_intra_recursive_halving.c), step by step:
-      pre-fold :163-195   even r < 2*rem sends everything to r+1, which computes
-                          tmp_results = x_r (+) x_{r-1} (its own data first)
-      halving  :197-283   newrank n, mask = pof2/2 .. 1, partner n ^ mask; the lower
-                          newrank keeps the low half of [send_idx, last_idx); received
-                          data is folded in as the second operand
-      final    :285-300   every participant copies its block; odd r < 2*rem sends
-                          block r-1 back to r-1."""
+def reduce_scatter_recursive_halving(rank_sendbufs: list[np.ndarray], recvcounts: list[int], esz: int,
+                                     dt: int, op: int) -> list[np.ndarray]:
+    """Each rank's recvbuf after MPI_Reduce_scatter's recursive halving
+    (reduce_scatter_intra_recursive_halving.c; the _block variant,
+    reduce_scatter_block_intra_recursive_halving.c:143-300, is this with equal
+    counts), step by step:
+      pre-fold   even r < 2*rem sends everything to r+1, which computes
+                 tmp_results = x_r (+) x_{r-1} (its own data first)
+      halving    newrank n, mask = pof2/2 .. 1, partner n ^ mask; the lower
+                 newrank keeps the low half of [send_idx, last_idx); received
+                 data is folded in as the second operand; newcnts[i] covers
+                 old ranks 2i and 2i+1 for i < rem
+      final      every participant copies its block; odd r < 2*rem sends
+                 block r-1 back to r-1."""
     p = len(rank_sendbufs)
-    nb = recvcount * esz
-    total = p * recvcount
-    res = [b.view(np.uint8).reshape(-1)[:p * nb].copy() for b in rank_sendbufs]   # tmp_results
+    total = sum(recvcounts)
+    disps = [sum(recvcounts[:i]) for i in range(p)]
+    res = [b.view(np.uint8).reshape(-1)[:total * esz].copy() for b in rank_sendbufs]   # tmp_results
     pof2 = _pof2(p)
     rem = p - pof2
     newrank = [0] * p
@@ -242,7 +245,7 @@ def reduce_scatter_block_recursive_halving(rank_sendbufs: list[np.ndarray], recv
     newcnts = []
     for i in range(pof2):
         old_i = i * 2 + 1 if i < rem else i + rem
-        newcnts.append(2 * recvcount if old_i < 2 * rem else recvcount)
+        newcnts.append(recvcounts[old_i] + recvcounts[old_i - 1] if old_i < 2 * rem else recvcounts[old_i])
     newdisps = [0] * pof2
     for i in range(1, pof2):
         newdisps[i] = newdisps[i - 1] + newcnts[i - 1]
@@ -278,10 +281,40 @@ def reduce_scatter_block_recursive_halving(rank_sendbufs: list[np.ndarray], recv
     out = [None] * p
     for r in range(p):
         if newrank[r] >= 0:
-            out[r] = res[r][r * nb:(r + 1) * nb].copy()
+            out[r] = res[r][disps[r] * esz:(disps[r] + recvcounts[r]) * esz].copy()
     for r in range(0, 2 * rem, 2):
-        out[r] = res[r + 1][r * nb:(r + 1) * nb].copy()
+        out[r] = res[r + 1][disps[r] * esz:(disps[r] + recvcounts[r]) * esz].copy()
     return out
+
+
+def reduce_scatter_block_recursive_halving(rank_sendbufs: list[np.ndarray], recvcount: int, esz: int,
+                                           dt: int, op: int) -> list[np.ndarray]:
+    """reduce_scatter_block_intra_recursive_halving.c:143-300 (equal counts)."""
+    return reduce_scatter_recursive_halving(rank_sendbufs, [recvcount] * len(rank_sendbufs), esz, dt, op)
+
+
+def reduce_scatter_pairwise(rank_sendbufs: list[np.ndarray], recvcounts: list[int], esz: int, dt: int,
+                            op: int) -> list[np.ndarray]:
+    """reduce_scatter_intra_pairwise.c: rank r's block = ((x_r + x_{r-1}) + x_{r-2}) + ..."""
+    p = len(rank_sendbufs)
+    disps = [sum(recvcounts[:i]) for i in range(p)]
+    send = [b.view(np.uint8).reshape(-1) for b in rank_sendbufs]
+    recv = [send[r][disps[r] * esz:(disps[r] + recvcounts[r]) * esz].copy() for r in range(p)]
+    for i in range(1, p):
+        for r in range(p):
+            src = (r - i + p) % p
+            tmp = send[src][disps[r] * esz:(disps[r] + recvcounts[r]) * esz].copy()
+            _red(tmp, recv[r], recvcounts[r], dt, op)
+    return recv
+
+
+def reduce_scatter_auto(rank_sendbufs: list[np.ndarray], recvcounts: list[int], esz: int, dt: int,
+                        op: int) -> list[np.ndarray]:
+    """MPI_Reduce_scatter with MPICH's choice for a builtin (commutative) op
+    (MPIR_Reduce_scatter_intra_auto, reduce_scatter.c)."""
+    if sum(recvcounts) * esz < RSB_COMMUTATIVE_LONG_MSG_SIZE:
+        return reduce_scatter_recursive_halving(rank_sendbufs, recvcounts, esz, dt, op)
+    return reduce_scatter_pairwise(rank_sendbufs, recvcounts, esz, dt, op)
 
 
 def reduce_scatter_block_auto(rank_sendbufs: list[np.ndarray], recvcount: int, esz: int, dt: int,

@@ -208,6 +208,54 @@ def test_reduce_reference_order(mpi, orc, cuda, t, op, p, inplace):
             mpi.comm_free(c)
 
 
+RSCASES = [("MPI_FLOAT", "MPI_SUM"), ("MPIX_C_FLOAT16", "MPI_SUM"), ("MPI_DOUBLE", "MPI_MIN"),
+           ("MPI_INT", "MPI_BXOR"), ("MPI_FLOAT_INT", "MPI_MAXLOC")]
+
+
+@pytest.mark.parametrize("t,op", RSCASES, ids=[f"{t}-{o}" for t, o in RSCASES])
+@pytest.mark.parametrize("p", [1, 2, 3, 5, 8])
+@pytest.mark.parametrize("inplace", [False, True])
+def test_reduce_scatter_reference_order(mpi, orc, cuda, t, op, p, inplace):
+    """MPIX_Reduce_scatter_hip with per-rank counts (zeros and a count larger
+    than its displacement included, so the in-place output overlaps the
+    rank's own block): recursive halving (short) and pairwise (long) vs the
+    step-by-step schedules."""
+    from oracle import schedules as S
+    torch = cuda
+    esz = T.elem_size(t)
+    dt, o = mpi.DATATYPES[t], mpi.OPS[op]
+    comms = mpi.comm_create_loopback(p)
+    try:
+        for scale, seed in ((1, p), (4096, 3 * p)):
+            rng = np.random.default_rng(seed)
+            counts = [int(c) * scale + int(rng.integers(0, 3)) for c in rng.integers(0, 9, p)]
+            if p > 2:
+                counts[1] = 0
+            if p > 1:
+                counts[-1] = sum(counts[:-1]) + 5
+            total = sum(counts)
+            xs = [T.to_bytes(T.gen(t, total, rng, op)) for _ in range(p)]
+            want = S.reduce_scatter_auto(xs, counts, esz, dt, o)
+            send = [torch.from_numpy(x.copy()).cuda() for x in xs]
+            recv = [s.clone() if inplace else torch.zeros(max(1, c) * esz, dtype=torch.uint8, device="cuda")
+                    for s, c in zip(send, counts)]
+            torch.cuda.synchronize()
+
+            def rank(r):
+                sb = mpi.MPI_IN_PLACE if inplace else send[r].data_ptr()
+                _ok(mpi, mpi.reduce_scatter(sb, recv[r].data_ptr(), counts, dt, o, comms[r],
+                                            mpi.MPIX_HIP_ALG_REFERENCE_ORDER))
+
+            run_ranks(rank, p)
+            torch.cuda.synchronize()
+            for r in range(p):
+                got = recv[r][:counts[r] * esz].cpu().numpy()
+                assert same(got, want[r], t), f"counts {counts} rank {r}"
+    finally:
+        for c in comms:
+            mpi.comm_free(c)
+
+
 def test_reduce_validation(mpi, cuda):
     torch = cuda
     comms = mpi.comm_create_loopback(2)

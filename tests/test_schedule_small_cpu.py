@@ -147,3 +147,39 @@ def test_reduce_short_binomial_plan_any_root(orc, t, op, p):
         for dst, src in binomial_plan(p):
             _red(orc, slots[src], slots[dst], count, t, op)
         assert np.array_equal(slots[0], want), f"root {root}"
+
+
+@pytest.mark.parametrize("t,op", CASES)
+@pytest.mark.parametrize("p", [2, 3, 5, 6, 8])
+def test_reduce_scatter_irregular_halving_plan(orc, t, op, p):
+    """MPI_Reduce_scatter (per-rank counts, zeros included) short path: the
+    same fold plan per block as the _block variant, over the simulation."""
+    from oracle import schedules as S
+    esz = T.elem_size(t)
+    rng = np.random.default_rng(p)
+    counts = [int(c) for c in rng.integers(0, 40, p)]
+    counts[p // 2] = 0
+    total = sum(counts)
+    disps = [sum(counts[:i]) for i in range(p)]
+    xs = _inputs(t, op, total, p, 5 * p)
+    want = S.reduce_scatter_auto(xs, counts, esz, DATATYPES[t], OPS[op])
+    for r in range(p):
+        pre, tree = halving_plan(p, r)
+        lo, hi = disps[r] * esz, (disps[r] + counts[r]) * esz
+        slots = [x[lo:hi].copy() for x in xs]
+        if counts[r]:
+            for dst, src in pre:
+                _red(orc, slots[src], slots[dst], counts[r], t, op)
+            got = tree_fold(orc, [slots[i] for i in tree], counts[r], t, op)
+        else:
+            got = slots[0]
+        assert np.array_equal(got, want[r]), f"p {p} rank {r} counts {counts}"
+
+
+def test_reduce_scatter_regular_counts_match_block_schedules(orc):
+    from oracle import schedules as S
+    p, rc = 5, 70000
+    xs = _inputs("MPI_FLOAT", "MPI_SUM", rc * p, p, 3)
+    a = S.reduce_scatter_pairwise(xs, [rc] * p, 4, DATATYPES["MPI_FLOAT"], OPS["MPI_SUM"])
+    b = S.reduce_scatter_block_pairwise(xs, rc, 4, DATATYPES["MPI_FLOAT"], OPS["MPI_SUM"])
+    assert all(np.array_equal(x, y) for x, y in zip(a, b))
