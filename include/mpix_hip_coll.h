@@ -78,6 +78,16 @@ int MPIX_Reduce_scatter_block_hip(const void *sendbuf, void *recvbuf, int recvco
 int MPIX_Reduce_scatter_hip(const void *sendbuf, void *recvbuf, const int recvcounts[], MPI_Datatype datatype,
                             MPI_Op op, MPIX_Hip_comm comm, int algorithm, void *hip_stream);
 
+/* MPI_Scan / MPI_Exscan semantics (scan.c, exscan.c; sendbuf may be
+ * MPI_IN_PLACE; the exscan's recvbuf at rank 0 is left untouched).  Reference
+ * order of the recursive doubling (scan_intra_recursive_doubling.c,
+ * exscan_intra_recursive_doubling.c); RCCL has no scan, so every algorithm
+ * value runs the reference order. */
+int MPIX_Scan_hip(const void *sendbuf, void *recvbuf, int count, MPI_Datatype datatype, MPI_Op op,
+                  MPIX_Hip_comm comm, int algorithm, void *hip_stream);
+int MPIX_Exscan_hip(const void *sendbuf, void *recvbuf, int count, MPI_Datatype datatype, MPI_Op op,
+                    MPIX_Hip_comm comm, int algorithm, void *hip_stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1025,3 +1025,118 @@ int MPIX_Reduce_scatter_hip(const void *sendbuf, void *recvbuf, const int recvco
     return reduce_scatter_common("MPIX_Reduce_scatter_hip", sendbuf, recvbuf, recvcounts, datatype, op, comm,
                                  algorithm, hip_stream);
 }
+
+/* ------------------------------------------------------------ Scan / Exscan
+ * On one node MPI_Scan is MPIR_Scan_intra_smp over node_comm, i.e. the
+ * recursive doubling of scan_intra_recursive_doubling.c:94-147; MPI_Exscan is
+ * exscan_intra_recursive_doubling.c:105-170.  At mask m rank r receives the
+ * partial scan of r ^ m and, when r > r ^ m, folds it into recvbuf as the
+ * second operand.  That partial scan is the full tree T(d) over
+ * z_j = x_{d ^ j}, j < m, d = r ^ m (each rank folds its partner's partial
+ * scan in second), so rank r's result is the chain
+ *     x_r (+) T(r ^ m_1) (+) T(r ^ m_2) ...      (m_i: set bits of r, increasing)
+ * and the exscan is the same chain without x_r (tests/test_schedule_small_cpu.py
+ * pins the plan against the step-by-step schedules).  MI355X form: every rank
+ * sends its vector to all higher ranks in ONE exchange (all xGMI links at
+ * once instead of log2(p) dependent rounds), then folds the trees and the
+ * chain on the device.  RCCL has no scan; MPIX_HIP_ALG_RCCL runs this too. */
+static int scan_common(const char *fc, const void *sendbuf, void *recvbuf, int count, MPI_Datatype datatype,
+                       MPI_Op op, MPIX_Hip_comm comm, void *hip_stream, int exclusive)
+{
+    struct MPIX_Hip_comm_s *c = comm;
+    int elem = 0, opidx = op & 0xf, rc, p, r, q, m, nx = 0, nr = 0, nparts = 0, cur = 0;
+    size_t esz, bytes, slot;
+    hipStream_t s;
+    xfer_t sends[MAX_XFER], recvs[MAX_XFER];
+    const void *chain[64], *ys[64];
+    const void *own;
+    char *scr = NULL;
+
+    if (!comm) {
+        MPIR_Err_set_detail("%s: null communicator", fc);
+        return MPIR_Err_return(fc, MPI_ERR_ARG);
+    }
+    /* the exscan's recvbuf is not significant at rank 0 */
+    rc = coll_check(fc, sendbuf, (exclusive && comm->rank == 0 && sendbuf != MPI_IN_PLACE) ? NULL : recvbuf, count,
+                    datatype, op, comm, &elem);
+    if (rc)
+        return MPIR_Err_return(fc, rc);
+    if (count == 0)
+        return MPI_SUCCESS;
+    if (hipGetDevice(&cur) == hipSuccess && cur != c->device)
+        (void) hipSetDevice(c->device);
+    s = hip_stream ? (hipStream_t) hip_stream : c->stream;
+    esz = MPIR_Hip_elem_size(elem);
+    bytes = (size_t) count * esz;
+    slot = (bytes + 255) & ~(size_t) 255;
+    p = c->size;
+    r = c->rank;
+    own = sendbuf == MPI_IN_PLACE ? recvbuf : sendbuf;
+    for (m = 1; m <= r; m <<= 1)
+        nparts += (r & m) != 0;
+    if (p > 1 && comm_scratch(c, (size_t) (r + nparts + 1) * slot, &scr)) {
+        MPIR_Err_set_detail("%s: scratch allocation failed", fc);
+        rc = MPI_ERR_NO_MEM;
+        goto done;
+    }
+    /* every rank's vector to all higher ranks; x_q lands in slot q */
+    for (q = 0; q < p; q++) {
+        if (q > r) {
+            sends[nx].buf = (void *) own;
+            sends[nx].bytes = bytes;
+            sends[nx++].peer = q;
+        } else if (q < r) {
+            recvs[nr].buf = scr + (size_t) q * slot;
+            recvs[nr].bytes = bytes;
+            recvs[nr++].peer = q;
+        }
+    }
+    if (p > 1)
+        TRY(group_exchange(c, sends, nx, recvs, nr, s));
+    nx = 0;
+    if (!exclusive)
+        chain[nx++] = own;
+    for (m = 1, q = 0; m <= r; m <<= 1) {
+        int d, j;
+        if (!(r & m))
+            continue;
+        d = r ^ m;
+        if (m == 1) {
+            chain[nx++] = scr + (size_t) d * slot;
+        } else {
+            char *t = scr + (size_t) (r + q++) * slot;
+            for (j = 0; j < m; j++)
+                ys[j] = scr + (size_t) (d ^ j) * slot;
+            TRY(fold_tree(ys, m, t, count, opidx, elem, s, fc));
+            chain[nx++] = t;
+        }
+    }
+    if (nx > 0) {
+        rc = MPIR_Hip_combine(chain, nx, recvbuf, (uint64_t) count, opidx, elem, MPIR_HIP_ORDER_CHAIN, s, 0);
+        if (rc) {
+            MPIR_Op_report_hip_error(fc, rc);
+            rc = MPI_ERR_OTHER;
+            goto done;
+        }
+    }
+    if (!hip_stream)
+        HIPTRY(hipStreamSynchronize(s));
+  done:
+    if (cur != c->device)
+        (void) hipSetDevice(cur);
+    return rc ? MPIR_Err_return(fc, rc) : MPI_SUCCESS;
+}
+
+int MPIX_Scan_hip(const void *sendbuf, void *recvbuf, int count, MPI_Datatype datatype, MPI_Op op,
+                  MPIX_Hip_comm comm, int algorithm, void *hip_stream)
+{
+    (void) algorithm;
+    return scan_common("MPIX_Scan_hip", sendbuf, recvbuf, count, datatype, op, comm, hip_stream, 0);
+}
+
+int MPIX_Exscan_hip(const void *sendbuf, void *recvbuf, int count, MPI_Datatype datatype, MPI_Op op,
+                    MPIX_Hip_comm comm, int algorithm, void *hip_stream)
+{
+    (void) algorithm;
+    return scan_common("MPIX_Exscan_hip", sendbuf, recvbuf, count, datatype, op, comm, hip_stream, 1);
+}

@@ -115,6 +115,7 @@ EXPORTED_SYMBOLS = [
     "MPIX_Hip_comm_get_unique_id", "MPIX_Hip_comm_create", "MPIX_Hip_comm_create_loopback",
     "MPIX_Hip_comm_free", "MPIX_Hip_comm_rank", "MPIX_Hip_comm_size",
     "MPIX_Allreduce_hip", "MPIX_Reduce_scatter_block_hip", "MPIX_Reduce_hip", "MPIX_Reduce_scatter_hip",
+    "MPIX_Scan_hip", "MPIX_Exscan_hip",
     # the HIP shim (include/mpir_hip_reduce.h)
     "MPIR_Hip_reduce", "MPIR_Hip_elem_size", "MPIR_Hip_has_kernel", "MPIR_Hip_is_device_ptr",
     "MPIR_Hip_memcpy", "MPIR_Hip_error_string", "MPIR_Hip_device_count",
@@ -157,7 +158,7 @@ def load(path: str | None = None) -> ctypes.CDLL:
     lib.MPIX_Hip_comm_create_loopback.restype = i32
     lib.MPIX_Hip_comm_free.argtypes = [ctypes.POINTER(vp)]
     lib.MPIX_Hip_comm_free.restype = i32
-    for name in ("MPIX_Allreduce_hip", "MPIX_Reduce_scatter_block_hip"):
+    for name in ("MPIX_Allreduce_hip", "MPIX_Reduce_scatter_block_hip", "MPIX_Scan_hip", "MPIX_Exscan_hip"):
         f = getattr(lib, name)
         f.argtypes = [vp, vp, i32, i32, i32, vp, i32, vp]
         f.restype = i32
@@ -249,6 +250,18 @@ def reduce(sendbuf, recvbuf, count: int, datatype: int, op: int, root: int, comm
            stream: int = 0) -> int:
     """MPIX_Reduce_hip (recvbuf significant at the root only; may be 0 elsewhere)."""
     return load().MPIX_Reduce_hip(ctypes.c_void_p(sendbuf), ctypes.c_void_p(recvbuf), count, datatype, op, root,
+                                  ctypes.c_void_p(comm), algorithm, ctypes.c_void_p(stream or None))
+
+
+def scan(sendbuf, recvbuf: int, count: int, datatype: int, op: int, comm, algorithm: int = 0,
+         stream: int = 0) -> int:
+    return load().MPIX_Scan_hip(ctypes.c_void_p(sendbuf), ctypes.c_void_p(recvbuf), count, datatype, op,
+                                ctypes.c_void_p(comm), algorithm, ctypes.c_void_p(stream or None))
+
+
+def exscan(sendbuf, recvbuf: int, count: int, datatype: int, op: int, comm, algorithm: int = 0,
+           stream: int = 0) -> int:
+    return load().MPIX_Exscan_hip(ctypes.c_void_p(sendbuf), ctypes.c_void_p(recvbuf), count, datatype, op,
                                   ctypes.c_void_p(comm), algorithm, ctypes.c_void_p(stream or None))
 
 

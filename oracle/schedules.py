@@ -337,3 +337,46 @@ def reduce_auto(rank_bufs: list[np.ndarray], count: int, esz: int, dt: int, op: 
     if count * esz > REDUCE_SHORT_MSG_SIZE and count >= _pof2(p):
         return allreduce_smp(rank_bufs, count, esz, dt, op)
     return reduce_binomial(rank_bufs, count, esz, dt, op, root=root)
+
+
+def _scan_rd(rank_sendbufs: list[np.ndarray], count: int, dt: int, op: int, exclusive: bool):
+    """The recursive-doubling prefix reductions, step by step.
+    scan_intra_recursive_doubling.c:94-147 (inclusive) and
+    exscan_intra_recursive_doubling.c:105-170 (exclusive), commutative op:
+    partial_scan starts as x_r; at mask m, r exchanges partial_scan with
+    r ^ m (< p) and folds the received one in as the SECOND operand; when
+    r > r ^ m it also folds it into recvbuf (exclusive: the first one is
+    copied).  Returns recvbuf per rank (None for rank 0 of an exscan)."""
+    p = len(rank_sendbufs)
+    ps = [b.view(np.uint8).reshape(-1).copy() for b in rank_sendbufs]
+    rb = [b.copy() if not exclusive else None for b in ps]
+    mask = 1
+    while mask < p:
+        sent = [x.copy() for x in ps]                  # MPIC_Sendrecv reads before this step's folds
+        for r in range(p):
+            dst = r ^ mask
+            if dst >= p:
+                continue
+            tmp = sent[dst]
+            _red(tmp.copy(), ps[r], count, dt, op)
+            if r > dst:
+                if exclusive and rb[r] is None:
+                    rb[r] = tmp.copy()
+                else:
+                    _red(tmp.copy(), rb[r], count, dt, op)
+        mask <<= 1
+    return rb
+
+
+def scan_recursive_doubling(rank_sendbufs: list[np.ndarray], count: int, esz: int, dt: int,
+                            op: int) -> list[np.ndarray]:
+    """MPI_Scan on one node: MPIR_Scan_intra_auto -> MPIR_Scan_intra_smp (node-
+    consecutive), whose single-node case is MPIR_Scan over node_comm, i.e. this
+    recursive doubling (scan.c, scan_intra_smp.c)."""
+    return _scan_rd(rank_sendbufs, count, dt, op, exclusive=False)
+
+
+def exscan_recursive_doubling(rank_sendbufs: list[np.ndarray], count: int, esz: int, dt: int,
+                              op: int) -> list[np.ndarray]:
+    """MPI_Exscan (MPIR_Exscan_intra_auto -> recursive doubling); rank 0 -> None."""
+    return _scan_rd(rank_sendbufs, count, dt, op, exclusive=True)

@@ -256,6 +256,51 @@ def test_reduce_scatter_reference_order(mpi, orc, cuda, t, op, p, inplace):
             mpi.comm_free(c)
 
 
+SCASES = [("MPI_FLOAT", "MPI_SUM"), ("MPIX_C_FLOAT16", "MPI_SUM"), ("MPI_DOUBLE", "MPI_MAX"),
+          ("MPI_LONG", "MPI_PROD"), ("MPI_2INT", "MPI_MINLOC"), ("MPI_C_FLOAT_COMPLEX", "MPI_SUM")]
+
+
+@pytest.mark.parametrize("t,op", SCASES, ids=[f"{t}-{o}" for t, o in SCASES])
+@pytest.mark.parametrize("p", [1, 2, 3, 5, 8])
+@pytest.mark.parametrize("inplace", [False, True])
+@pytest.mark.parametrize("exclusive", [False, True])
+def test_scan_reference_order(mpi, orc, cuda, t, op, p, inplace, exclusive):
+    """MPIX_Scan_hip / MPIX_Exscan_hip vs the step-by-step recursive doubling;
+    the exscan leaves rank 0's recvbuf untouched."""
+    from oracle import schedules as S
+    torch = cuda
+    esz = T.elem_size(t)
+    dt, o = mpi.DATATYPES[t], mpi.OPS[op]
+    fn = mpi.exscan if exclusive else mpi.scan
+    sim = S.exscan_recursive_doubling if exclusive else S.scan_recursive_doubling
+    comms = mpi.comm_create_loopback(p)
+    try:
+        for count, seed in ((5, p), ((1 << 17) + 3, 3 * p)):
+            rng = np.random.default_rng(seed)
+            xs = [T.to_bytes(T.gen(t, count, rng, op)) for _ in range(p)]
+            want = sim(xs, count, esz, dt, o)
+            send = [torch.from_numpy(x.copy()).cuda() for x in xs]
+            recv = [s.clone() if inplace else torch.full_like(s, 0xA5) for s in send]
+            before0 = recv[0].clone()
+            torch.cuda.synchronize()
+
+            def rank(r):
+                sb = mpi.MPI_IN_PLACE if inplace else send[r].data_ptr()
+                _ok(mpi, fn(sb, recv[r].data_ptr(), count, dt, o, comms[r], mpi.MPIX_HIP_ALG_REFERENCE_ORDER))
+
+            run_ranks(rank, p)
+            torch.cuda.synchronize()
+            for r in range(p):
+                got = recv[r].cpu().numpy()
+                if exclusive and r == 0:
+                    assert torch.equal(recv[0], before0), "exscan wrote rank 0's recvbuf"
+                    continue
+                assert same(got, want[r], t), f"count {count} rank {r}"
+    finally:
+        for c in comms:
+            mpi.comm_free(c)
+
+
 def test_reduce_validation(mpi, cuda):
     torch = cuda
     comms = mpi.comm_create_loopback(2)

@@ -183,3 +183,39 @@ def test_reduce_scatter_regular_counts_match_block_schedules(orc):
     a = S.reduce_scatter_pairwise(xs, [rc] * p, 4, DATATYPES["MPI_FLOAT"], OPS["MPI_SUM"])
     b = S.reduce_scatter_block_pairwise(xs, rc, 4, DATATYPES["MPI_FLOAT"], OPS["MPI_SUM"])
     assert all(np.array_equal(x, y) for x, y in zip(a, b))
+
+
+def scan_plan(r):
+    """Device plan for rank r's scan: the partial scans r receives in the
+    recursive doubling are, per set bit m of r (increasing), the full tree
+    T(d) over z_j = x_{d ^ j}, j < m, with d = r ^ m; the result is the chain
+    x_r (+) T(d_1) (+) T(d_2) ... (exscan: the chain without x_r)."""
+    out, m = [], 1
+    while m <= r:
+        if r & m:
+            d = r ^ m
+            out.append([d ^ j for j in range(m)])
+        m <<= 1
+    return out
+
+
+@pytest.mark.parametrize("t,op", CASES)
+@pytest.mark.parametrize("p", [1, 2, 3, 5, 6, 8, 13])
+@pytest.mark.parametrize("exclusive", [False, True])
+def test_scan_plan(orc, t, op, p, exclusive):
+    from oracle import schedules as S
+    esz = T.elem_size(t)
+    count = 7
+    xs = _inputs(t, op, count, p, 11 * p)
+    fn = S.exscan_recursive_doubling if exclusive else S.scan_recursive_doubling
+    want = fn(xs, count, esz, DATATYPES[t], OPS[op])
+    for r in range(p):
+        parts = [tree_fold(orc, [xs[i].copy() for i in blk], count, t, op) for blk in scan_plan(r)]
+        chain = parts if exclusive else [xs[r].copy()] + parts
+        if not chain:
+            assert r == 0 and want[0] is None
+            continue
+        acc = chain[0].copy()
+        for x in chain[1:]:
+            _red(orc, x, acc, count, t, op)
+        assert np.array_equal(acc, want[r]), f"rank {r}"
