@@ -109,6 +109,102 @@ __global__ __launch_bounds__(kThreads) void k_reduce_tile(TileArgs<T> args) {
     }
 }
 
+// inbuf misaligned relative to inoutbuf: (in - io) mod 16 = delta != 0, the
+// case of a schedule step whose tmp_buf and recvbuf sub-ranges start at
+// different offsets mod 16.  inoutbuf is peeled to 16 B alignment as in
+// k_reduce_tile and streamed the same way; inbuf is read as ALIGNED 16-byte
+// vectors (lane k loads vector k of the tile, starting delta bytes before the
+// operand) and each lane rebuilds its 16 operand bytes from its own vector and
+// its neighbour's: a wavefront shuffle (ds_bpermute) hands lane k the vector
+// of lane k+1, lane 63 of each wave loads that one itself, and
+// v_alignbyte funnels the two at byte offset delta.  The in-buffer descriptor
+// ends at the last 16 B vector holding operand bytes; loads past it read 0.
+template <int D>
+__device__ __forceinline__ u32x4 funnel_d(const uint32_t (&w)[8], uint32_t sh) {
+    u32x4 r;
+    r.x = __builtin_amdgcn_alignbyte(w[D + 1], w[D + 0], sh);
+    r.y = __builtin_amdgcn_alignbyte(w[D + 2], w[D + 1], sh);
+    r.z = __builtin_amdgcn_alignbyte(w[D + 3], w[D + 2], sh);
+    r.w = __builtin_amdgcn_alignbyte(w[D + 4], w[D + 3], sh);
+    return r;
+}
+
+// bytes [delta, delta + 16) of the 32-byte concatenation lo:hi (delta uniform)
+__device__ __forceinline__ u32x4 funnel16(u32x4 lo, u32x4 hi, uint32_t delta) {
+    const uint32_t w[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+    const uint32_t sh = delta & 3;
+    switch (delta >> 2) {
+    case 0: return funnel_d<0>(w, sh);
+    case 1: return funnel_d<1>(w, sh);
+    case 2: return funnel_d<2>(w, sh);
+    default: return funnel_d<3>(w, sh);
+    }
+}
+
+template <class T>
+struct ShiftArgs {
+    TileArgs<T> t;      // t.in is unused: the in region is in_al + delta
+    const char *in_al;  // in region start rounded down to 16 B
+    uint32_t delta;     // 1..15
+};
+
+template <class Op, class T>
+__global__ __launch_bounds__(kThreads) void k_reduce_shift(ShiftArgs<T> args) {
+    const TileArgs<T> &ta = args.t;
+    const uint64_t base = (uint64_t)blockIdx.x * kTileBytes;
+    if (base < ta.vbytes) {
+        const uint64_t left = ta.vbytes - base;
+        const int nrec = (int)(left < kTileBytes ? left : kTileBytes);
+        // operand bytes from in_al + base on, rounded up to whole 16 B vectors: the
+        // range check of a dwordx4 load is per access, so the vector holding the
+        // operand's last bytes must be fully in range (an aligned 16 B block never
+        // crosses a page, so its bytes past the operand are mapped; they are unused)
+        const uint64_t in_left = (args.delta + left + 15) & ~(uint64_t)15;
+        const int nrec_in = (int)(in_left < kTileBytes + 16 ? in_left : kTileBytes + 16);
+        __amdgpu_buffer_rsrc_t rin = __builtin_amdgcn_make_buffer_rsrc((void *)(args.in_al + base), 0, nrec_in, 0x00020000);
+        __amdgpu_buffer_rsrc_t rio = __builtin_amdgcn_make_buffer_rsrc((void *)(ta.io + base), 0, nrec, 0x00020000);
+        const bool last_lane = (threadIdx.x & 63) == 63;
+        u32x4 a[kVecPerLane], b[kVecPerLane], n63[kVecPerLane];
+#pragma unroll
+        for (int u = 0; u < kVecPerLane; ++u) {
+            const int off = (u * kThreads + (int)threadIdx.x) * 16;
+            a[u] = __builtin_amdgcn_raw_buffer_load_b128(rio, off, 0, kCachePolicyNT);
+            b[u] = __builtin_amdgcn_raw_buffer_load_b128(rin, off, 0, kCachePolicyNT);
+            // lane 63's neighbour vector: every lane issues the load, the others
+            // at an offset past the descriptor's range (returns 0, no memory
+            // request) -- a branch here would make the compiler drain vmcnt
+            n63[u] = __builtin_amdgcn_raw_buffer_load_b128(rin, last_lane ? off + 16 : 0x40000000, 0, kCachePolicyNT);
+        }
+#pragma unroll
+        for (int u = 0; u < kVecPerLane; ++u) {
+            const int off = (u * kThreads + (int)threadIdx.x) * 16;
+            // neighbour from the shuffle, OR the lane-63 load (0 on every other
+            // lane): branch-free, so the load cannot be sunk into a branch
+            const uint32_t keep = last_lane ? 0u : ~0u;
+            u32x4 nb;
+            nb.x = (__shfl_down(b[u].x, 1, 64) & keep) | n63[u].x;
+            nb.y = (__shfl_down(b[u].y, 1, 64) & keep) | n63[u].y;
+            nb.z = (__shfl_down(b[u].z, 1, 64) & keep) | n63[u].z;
+            nb.w = (__shfl_down(b[u].w, 1, 64) & keep) | n63[u].w;
+            __builtin_amdgcn_raw_buffer_store_b128(combine16<Op, T>(a[u], funnel16(b[u], nb, args.delta)), rio, off,
+                                                   0, kCachePolicyNT);
+        }
+    }
+    if (blockIdx.x == 0) {
+        Op op;
+        const unsigned t = threadIdx.x;
+        if (t < ta.nhead) {
+            T x = ta.head_io[t], y;
+            __builtin_memcpy(&y, reinterpret_cast<const char *>(ta.head_in) + t * sizeof(T), sizeof(T));
+            ta.head_io[t] = op(x, y);
+        } else if (t >= 64 && t - 64 < ta.ntail) {
+            T x = ta.tail_io[t - 64], y;
+            __builtin_memcpy(&y, reinterpret_cast<const char *>(ta.tail_in) + (t - 64) * sizeof(T), sizeof(T));
+            ta.tail_io[t - 64] = op(x, y);
+        }
+    }
+}
+
 // General path: inbuf and inoutbuf differ in alignment mod 16 (sub-range
 // displacements of arbitrary element counts), or elements are not even
 // naturally aligned.  Element-granular, coalesced, grid-stride.
@@ -159,6 +255,28 @@ hipError_t launch_reduce(const void *in_, void *io_, uint64_t count, hipStream_t
         uint64_t grid = (vbytes + kTileBytes - 1) / kTileBytes;
         if (grid == 0) grid = 1;
         hipLaunchKernelGGL((k_reduce_tile<Op, T>), dim3((unsigned)grid), dim3(kThreads), 0, s, a);
+    } else if ((ao % alignof(T) == 0) && head0 % sizeof(T) == 0 && nbytes >= 2 * kTileBytes) {
+        // inoutbuf element-aligned, inbuf at any other offset mod 16: the
+        // aligned-load + shuffle + funnel tile kernel (small counts stay
+        // on the element kernel, where a launch's setup dominates anyway)
+        const uint64_t head_bytes = head0;
+        const uint64_t rest = nbytes - head_bytes;
+        const uint64_t vbytes = rest & ~(uint64_t)15;
+        ShiftArgs<T> a;
+        a.t.in = nullptr;
+        a.t.io = io + head_bytes;
+        a.t.vbytes = vbytes;
+        a.t.head_in = reinterpret_cast<const T *>(in);
+        a.t.head_io = reinterpret_cast<T *>(io);
+        a.t.nhead = (uint32_t)(head_bytes / sizeof(T));
+        a.t.tail_in = reinterpret_cast<const T *>(in + head_bytes + vbytes);
+        a.t.tail_io = reinterpret_cast<T *>(io + head_bytes + vbytes);
+        a.t.ntail = (uint32_t)((rest - vbytes) / sizeof(T));
+        const uintptr_t vin = ai + head_bytes;
+        a.delta = (uint32_t)(vin & 15);
+        a.in_al = reinterpret_cast<const char *>(vin - a.delta);
+        uint64_t grid = (vbytes + kTileBytes - 1) / kTileBytes;
+        hipLaunchKernelGGL((k_reduce_shift<Op, T>), dim3((unsigned)grid), dim3(kThreads), 0, s, a);
     } else {
         uint64_t grid = (count + kThreads - 1) / kThreads;
         if (grid > 4096) grid = 4096;

@@ -111,6 +111,25 @@ def test_alignment_offsets(mpi, orc, cuda, t):
             run_pair(mpi, orc, cuda, op, t, n, 100 + n + off_in, off_in, off_io)
 
 
+SHIFT_CASES = [("MPI_SUM", "MPI_FLOAT"), ("MPI_MAX", "MPI_DOUBLE"), ("MPI_SUM", "MPIX_C_FLOAT16"),
+               ("MPI_BXOR", "MPI_UNSIGNED_CHAR"), ("MPI_PROD", "MPI_INT64_T"), ("MPI_SUM", "MPI_C_FLOAT_COMPLEX"),
+               ("MPI_MINLOC", "MPI_DOUBLE_INT"), ("MPI_SUM", "MPI_LONG_DOUBLE"), ("MPI_LXOR", "MPI_SHORT")]
+
+
+@pytest.mark.parametrize("op,t", SHIFT_CASES, ids=[f"{o}-{t}" for o, t in SHIFT_CASES])
+def test_relative_misalignment_tile_path(mpi, orc, cuda, op, t):
+    """Counts of several tiles with inbuf at every offset mod 16 relative to
+    inoutbuf: the aligned-load + wavefront-shuffle + funnel kernel
+    (k_reduce_shift), its head / tail elements and ragged last tile."""
+    esz = T.elem_size(t)
+    n = (3 * 16384 + 37 * 16) // esz + 3
+    for off_io in (0, esz, 16 - esz if esz < 16 else 0):
+        for off_in in range(0, 16):
+            if (off_in - off_io) % 16 == 0:
+                continue
+            run_pair(mpi, orc, cuda, op, t, n, 7 * off_in + off_io, off_in, off_io)
+
+
 def test_golden_kat_fold_on_gpu(mpi, cuda):
     """The reference's own known-answer tests, folded on the GPU, bit for bit."""
     torch = cuda
