@@ -91,5 +91,43 @@ int main(int argc, char **argv) {
         const double gbs = 3.0 * bytes / med / 1e9;
         printf("  %-30s median %8.2f us  %7.0f GB/s  frac %.3f\n", v.name.c_str(), med * 1e6, gbs, gbs / 8000.0);
     }
+
+    // data content: the same aligned fp32 kernel with zero operands.  MPI_BAND
+    // with an all-zero inbuf keeps inout at zero, so every round sees the same bytes.
+    {
+        char *zi, *zo, *ri, *ro;
+        CK(hipMalloc(&zi, bytes)); CK(hipMalloc(&zo, bytes));
+        CK(hipMalloc(&ri, bytes)); CK(hipMalloc(&ro, bytes));
+        CK(hipMemset(zi, 0, bytes)); CK(hipMemset(zo, 0, bytes));
+        std::vector<uint32_t> r(bytes / 4);
+        uint64_t x = 88172645463325252ull;
+        for (auto &w : r) { x ^= x << 13; x ^= x >> 7; x ^= x << 17; w = (uint32_t)x; }
+        CK(hipMemcpy(ri, r.data(), bytes, hipMemcpyHostToDevice));
+        CK(hipMemcpy(ro, r.data(), bytes, hipMemcpyHostToDevice));
+        // every variant leaves its inout unchanged: x & x = x, 0 & 0 = 0, x | 0 = x
+        struct D { const char *name; char *i, *o; hipError_t (*fn)(const void *, void *, uint64_t, hipStream_t);
+                   std::vector<float> ms; };
+        std::vector<D> ds = {{"u32 BAND random / random", ri, ro, &launch_reduce<OpBand, uint32_t>, {}},
+                             {"u32 BAND zero / zero", zi, zo, &launch_reduce<OpBand, uint32_t>, {}},
+                             {"u32 BOR zero in / random inout", zi, ro, &launch_reduce<OpBor, uint32_t>, {}}};
+        for (int rr = -2; rr < rounds; ++rr) {
+            for (auto &d : ds) {
+                CK(hipEventRecord(e0, st));
+                CK(d.fn(d.i, d.o, bytes / 4, st));
+                CK(hipEventRecord(e1, st));
+                CK(hipEventSynchronize(e1));
+                float ms;
+                CK(hipEventElapsedTime(&ms, e0, e1));
+                if (rr >= 0) d.ms.push_back(ms);
+            }
+        }
+        printf("data content (aligned k_reduce_tile, u32):\n");
+        for (auto &d : ds) {
+            std::sort(d.ms.begin(), d.ms.end());
+            const double med = d.ms[d.ms.size() / 2] * 1e-3;
+            const double gbs = 3.0 * bytes / med / 1e9;
+            printf("  %-30s median %8.2f us  %7.0f GB/s  frac %.3f\n", d.name, med * 1e6, gbs, gbs / 8000.0);
+        }
+    }
     return 0;
 }
