@@ -258,6 +258,9 @@ def main():
             "api": "MPI_Reduce_local (C ABI, synchronous)",
             "parallelism": "replica-per-gpu (no data-path collective)",
         },
+        # the synchronous call per GPU (launch + completion included) against the HBM peak
+        "per_gpu": {"GiBps": round(value / world, 1),
+                    "frac_of_hbm_peak": round(value / world * GIB / HBM_PEAK_BPS, 4)},
     }
 
     if not args.no_extras:
