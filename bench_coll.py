@@ -9,9 +9,9 @@ launched with WORLD_SIZE > 1; its results land in bench.py's JSON line under
 
 Per rank: builds an RCCL communicator through the C ABI (MPIX_Hip_comm_create;
 unique id exchanged over a TCPStore on 127.0.0.1), then
-  1. a self-check on the real xGMI transport: a reference-order
-     MPIX_Allreduce_hip (fp32 SUM) and MPIX_Reduce_scatter_block_hip (fp16 SUM)
-     on deterministic finite per-rank inputs, compared bit for bit with numpy
+  1. a self-check on the real xGMI transport: reference-order
+     MPIX_Allreduce_hip, MPIX_Reduce_hip, MPIX_Scan_hip, MPIX_Exscan_hip (fp32 SUM)
+     and MPIX_Reduce_scatter_block_hip (fp16 SUM) on deterministic finite per-rank inputs, compared bit for bit with numpy
      evaluating the same association (recursive-halving tree per block /
      pairwise chain -- see expect_* below; numpy's fp32/fp16 adds round like
      the reference's).  The full parity suite against the oracle lives in
@@ -73,6 +73,37 @@ def expect_reduce_scatter_block(xs, rank: int, rcount: int):
     acc = xs[rank][sl].copy()
     for i in range(1, p):
         acc = acc + xs[(rank - i) % p][sl]
+    return acc
+
+
+def _tree(vs):
+    """((v0+v1)+(v2+v3))+... (left operand first; len(vs) a power of two)."""
+    v = [x.copy() for x in vs]
+    step = 1
+    while step < len(v):
+        for j in range(0, len(v), 2 * step):
+            v[j] = v[j] + v[j + step]
+        step *= 2
+    return v[0]
+
+
+def expect_scan(xs, rank: int, exclusive: bool = False):
+    """Recursive-doubling scan order (scan_intra_recursive_doubling.c:94-147,
+    exscan_intra_recursive_doubling.c:105-170): rank r's result is the chain
+    x_r + T(r^m_1) + T(r^m_2) + ... over the set bits m of r (increasing),
+    T(d) the tree over x_{d^j}, j < m (exscan: without x_r; None at rank 0)."""
+    parts, m = [], 1
+    while m <= rank:
+        if rank & m:
+            d = rank ^ m
+            parts.append(_tree([xs[d ^ j] for j in range(m)]))
+        m <<= 1
+    chain = parts if exclusive else [xs[rank]] + parts
+    if not chain:
+        return None
+    acc = chain[0].copy()
+    for x in chain[1:]:
+        acc = acc + x
     return acc
 
 
@@ -145,11 +176,31 @@ def main():
     assert m.reduce_scatter_block(hsend.data_ptr(), hrecv.data_ptr(), rcount, F16, SUM, C, REF) == 0
     ok_rs = bool(np.array_equal(hrecv.cpu().numpy().view(np.uint16),
                                 expect_reduce_scatter_block(hs, rank, rcount).view(np.uint16)))
-    flags = torch.tensor([float(ok_ar), float(ok_rs)], dtype=torch.float64, device="cuda")
-    assert m.allreduce(m.MPI_IN_PLACE, flags.data_ptr(), 2, m.MPI_DOUBLE, m.MPI_MIN, C, RCCL) == 0
+    # MPI_Reduce to the last rank: the long path's block values are the allreduce's
+    root = world - 1
+    rrecv = torch.zeros_like(send)
+    torch.cuda.synchronize()
+    assert m.reduce(send.data_ptr(), rrecv.data_ptr() if rank == root else 0, n, F32, SUM, root, C, REF) == 0
+    ok_rd = bool(np.array_equal(rrecv.cpu().numpy().view(np.uint32), expect_allreduce(xs).view(np.uint32))) \
+        if (pof2 and rank == root) else True
+    # MPI_Scan / MPI_Exscan (recursive-doubling order)
+    srecv = torch.zeros_like(send)
+    erecv = torch.zeros_like(send)
+    torch.cuda.synchronize()
+    assert m.scan(send.data_ptr(), srecv.data_ptr(), n, F32, SUM, C, REF) == 0
+    assert m.exscan(send.data_ptr(), erecv.data_ptr(), n, F32, SUM, C, REF) == 0
+    ok_sc = bool(np.array_equal(srecv.cpu().numpy().view(np.uint32), expect_scan(xs, rank).view(np.uint32)))
+    ex = expect_scan(xs, rank, exclusive=True)
+    ok_ex = True if ex is None else bool(np.array_equal(erecv.cpu().numpy().view(np.uint32), ex.view(np.uint32)))
+    flags = torch.tensor([float(ok_ar), float(ok_rs), float(ok_rd), float(ok_sc), float(ok_ex)],
+                         dtype=torch.float64, device="cuda")
+    assert m.allreduce(m.MPI_IN_PLACE, flags.data_ptr(), 5, m.MPI_DOUBLE, m.MPI_MIN, C, RCCL) == 0
     out["parity_reference_order"] = {
         "allreduce_fp32_sum_bitexact": bool(flags[0].item() == 1.0) if pof2 else "not checked (non-pof2 N)",
         "reduce_scatter_block_fp16_sum_bitexact": bool(flags[1].item() == 1.0),
+        "reduce_fp32_sum_bitexact": bool(flags[2].item() == 1.0) if pof2 else "not checked (non-pof2 N)",
+        "scan_fp32_sum_bitexact": bool(flags[3].item() == 1.0),
+        "exscan_fp32_sum_bitexact": bool(flags[4].item() == 1.0),
         "checker": "numpy, same association (full oracle parity: tests/test_coll_*)"}
 
     # ---- 2. timing

@@ -26,3 +26,29 @@ def test_reduce_scatter_expectation_matches_schedule(orc, p):
     want = S.reduce_scatter_block_pairwise([h.view(np.uint8) for h in hs], rc, 2, MPIX_C_FLOAT16, MPI_SUM)
     for r in range(p):
         assert np.array_equal(B.expect_reduce_scatter_block(hs, r, rc).view(np.uint8), want[r][:rc * 2])
+
+
+@pytest.mark.parametrize("p", [1, 2, 3, 4, 8])
+@pytest.mark.parametrize("exclusive", [False, True])
+def test_scan_expectation_matches_schedule(orc, p, exclusive):
+    from oracle import schedules as S
+    n = 1031
+    xs = [np.random.default_rng(5 + r).uniform(-1, 1, n).astype(np.float32) for r in range(p)]
+    fn = S.exscan_recursive_doubling if exclusive else S.scan_recursive_doubling
+    want = fn([x.view(np.uint8) for x in xs], n, 4, MPI_FLOAT, MPI_SUM)
+    for r in range(p):
+        got = B.expect_scan(xs, r, exclusive)
+        if want[r] is None:
+            assert got is None
+        else:
+            assert np.array_equal(got.view(np.uint8), want[r])
+
+
+@pytest.mark.parametrize("p", [2, 4, 8])
+def test_reduce_expectation_matches_schedule(orc, p):
+    """The bench's Reduce check (root p-1, long message) reuses the allreduce closed form."""
+    from oracle import schedules as S
+    n = (1 << 16) + 3
+    xs = [np.random.default_rng(77 + r).uniform(-1, 1, n).astype(np.float32) for r in range(p)]
+    want = S.reduce_auto([x.view(np.uint8) for x in xs], n, 4, MPI_FLOAT, MPI_SUM, p - 1)
+    assert np.array_equal(B.expect_allreduce(xs).view(np.uint8), want)
