@@ -11,116 +11,22 @@
 #include <string.h>
 
 #include "mpir_hip_reduce.h"
-#include "reduce_kernels.hpp"
+#include "kernel_table.hpp"
 
 using namespace mpir_hip;
 
 namespace {
 
-typedef hipError_t (*launch_fn)(const void *, void *, uint64_t, hipStream_t);
+// Kernel tables (kernel_table.hpp), filled by the registration units
+// reg_*.hip at static-initialisation time; zero-initialised storage here.
+}  // namespace
 
-typedef hipError_t (*any_fn)(const void *const *, int, int, void *, uint64_t, hipStream_t);
-
-// g_table: the single-operand MPIR_Reduce_local kernel per (op, element class);
-// any: the one-pass n-operand combine of the same pair (MPIR_Hip_combine's
-// general path).  REPLACE has no n-operand form (its fold is the last operand).
-struct Entry { launch_fn fn; any_fn any; };
+namespace mpir_hip {
 Entry g_table[MPIR_HIP_NOPS][MPIR_HIP_NELEMS];
-
-template <class Op, class T>
-void reg(int op, int elem) {
-    g_table[op][elem].fn = &launch_reduce<Op, T>;
-    if constexpr (!__is_same(Op, OpReplace)) g_table[op][elem].any = &launch_combine_any<Op, T>;
-}
-template <class Op, class T, int EPL = 2>
-void reg_wide(int op, int elem) {
-    g_table[op][elem].fn = &launch_reduce_wide<Op, T, EPL>;
-    g_table[op][elem].any = &launch_combine_any<Op, T>;
-}
-
-// Integer element classes and their device types.
-#define FOR_INTS(X) \
-    X(MPIR_HIP_I8, int8_t) X(MPIR_HIP_U8, uint8_t) X(MPIR_HIP_I16, int16_t) X(MPIR_HIP_U16, uint16_t) \
-    X(MPIR_HIP_I32, int32_t) X(MPIR_HIP_U32, uint32_t) X(MPIR_HIP_I64, int64_t) X(MPIR_HIP_U64, uint64_t)
-#define FOR_REALS(X) X(MPIR_HIP_F16, f16) X(MPIR_HIP_F32, float) X(MPIR_HIP_F64, double)
-#define FOR_CPLX(X) X(MPIR_HIP_CF32, cf32) X(MPIR_HIP_CF64, cf64)
-#define FOR_PAIRS(X) \
-    X(MPIR_HIP_P2INT, p2int) X(MPIR_HIP_PFLOATINT, pfloatint) X(MPIR_HIP_PLONGINT, plongint) \
-    X(MPIR_HIP_PSHORTINT, pshortint) X(MPIR_HIP_PDOUBLEINT, pdoubleint)
-
-struct TableInit {
-    TableInit() {
-        memset(g_table, 0, sizeof(g_table));
-        // SUM / PROD: C_INTEGER, FORTRAN_INTEGER, FLOATING_POINT (+EXTRA: char, _Float16), COMPLEX
-#define X(E, T) reg<OpSum, T>(MPIR_HIP_OP_SUM, E); reg<OpProd, T>(MPIR_HIP_OP_PROD, E);
-        FOR_INTS(X) FOR_REALS(X) FOR_CPLX(X)
-#undef X
-        // MAX / MIN: integers and reals, no complex
-#define X(E, T) reg<OpMax, T>(MPIR_HIP_OP_MAX, E); reg<OpMin, T>(MPIR_HIP_OP_MIN, E);
-        FOR_INTS(X) FOR_REALS(X)
-#undef X
-        // LAND / LOR: integers (+ _Bool as u8); LXOR also reals (oplxor.c:66-67)
-#define X(E, T) reg<OpLand, T>(MPIR_HIP_OP_LAND, E); reg<OpLor, T>(MPIR_HIP_OP_LOR, E); \
-                reg<OpLxor, T>(MPIR_HIP_OP_LXOR, E);
-        FOR_INTS(X)
-#undef X
-#define X(E, T) reg<OpLxor, T>(MPIR_HIP_OP_LXOR, E);
-        FOR_REALS(X)
-#undef X
-        // BAND / BOR / BXOR: integers and byte
-#define X(E, T) reg<OpBand, T>(MPIR_HIP_OP_BAND, E); reg<OpBor, T>(MPIR_HIP_OP_BOR, E); \
-                reg<OpBxor, T>(MPIR_HIP_OP_BXOR, E);
-        FOR_INTS(X)
-#undef X
-        // MAXLOC / MINLOC: pair types
-#define X(E, T) reg<OpMaxloc, T>(MPIR_HIP_OP_MAXLOC, E); reg<OpMinloc, T>(MPIR_HIP_OP_MINLOC, E);
-        FOR_PAIRS(X)
-#undef X
-        // long double: FLOATING_POINT (SUM, PROD, MAX, MIN, LXOR), its _Complex
-        // (SUM, PROD), MPI_LONG_DOUBLE_INT (MAXLOC, MINLOC) -- x87 in software
-        reg<OpSum, x80>(MPIR_HIP_OP_SUM, MPIR_HIP_F80);
-        reg<OpProd, x80>(MPIR_HIP_OP_PROD, MPIR_HIP_F80);
-        reg<OpMax, x80>(MPIR_HIP_OP_MAX, MPIR_HIP_F80);
-        reg<OpMin, x80>(MPIR_HIP_OP_MIN, MPIR_HIP_F80);
-        reg<OpLxor, x80>(MPIR_HIP_OP_LXOR, MPIR_HIP_F80);
-        reg_wide<OpSum, cx80>(MPIR_HIP_OP_SUM, MPIR_HIP_CF80);
-        reg_wide<OpProd, cx80, 1>(MPIR_HIP_OP_PROD, MPIR_HIP_CF80);
-        reg_wide<OpMaxloc, pldint>(MPIR_HIP_OP_MAXLOC, MPIR_HIP_PLDOUBLEINT);
-        reg_wide<OpMinloc, pldint>(MPIR_HIP_OP_MINLOC, MPIR_HIP_PLDOUBLEINT);
-        // REPLACE: a byte copy for every class (MPIR_Localcopy of a basic type)
-        for (int e = 1; e < MPIR_HIP_NELEMS; ++e) reg<OpReplace, uint8_t>(MPIR_HIP_OP_REPLACE, e);
-    }
-} g_table_init;
-
-// ---- multi-operand (fused schedule) combines: [op][elem][order][P = 2, 4, 8]
-typedef hipError_t (*multi_fn)(const void *const *, void *, uint64_t, hipStream_t);
 multi_fn g_multi[MPIR_HIP_NOPS][MPIR_HIP_NELEMS][2][3];
+}  // namespace mpir_hip
 
-template <class Op, class T>
-void reg_multi(int op, int elem) {
-    g_multi[op][elem][0][0] = &launch_combine_p<Op, T, 2, true>;
-    g_multi[op][elem][0][1] = &launch_combine_p<Op, T, 4, true>;
-    g_multi[op][elem][0][2] = &launch_combine_p<Op, T, 8, true>;
-    g_multi[op][elem][1][0] = &launch_combine_p<Op, T, 2, false>;
-    g_multi[op][elem][1][1] = &launch_combine_p<Op, T, 4, false>;
-    g_multi[op][elem][1][2] = &launch_combine_p<Op, T, 8, false>;
-}
-
-struct MultiInit {
-    MultiInit() {
-        memset(g_multi, 0, sizeof(g_multi));
-        // the ops the reduction collectives are built on (configs 4-5): SUM/PROD/MAX/MIN
-        // over integers and reals (+ complex SUM/PROD).  Other (op, type) pairs run
-        // the schedule step by step through MPIR_Hip_reduce.
-#define X(E, T) reg_multi<OpSum, T>(MPIR_HIP_OP_SUM, E); reg_multi<OpProd, T>(MPIR_HIP_OP_PROD, E); \
-                reg_multi<OpMax, T>(MPIR_HIP_OP_MAX, E); reg_multi<OpMin, T>(MPIR_HIP_OP_MIN, E);
-        X(MPIR_HIP_I32, int32_t) X(MPIR_HIP_U32, uint32_t) X(MPIR_HIP_I64, int64_t) X(MPIR_HIP_U64, uint64_t)
-        X(MPIR_HIP_F16, f16) X(MPIR_HIP_F32, float) X(MPIR_HIP_F64, double)
-#undef X
-        reg_multi<OpSum, cf32>(MPIR_HIP_OP_SUM, MPIR_HIP_CF32);
-        reg_multi<OpSum, cf64>(MPIR_HIP_OP_SUM, MPIR_HIP_CF64);
-    }
-} g_multi_init;
+namespace {
 
 const size_t g_elem_size[MPIR_HIP_NELEMS] = {
     0, 1, 1, 2, 2, 4, 4, 8, 8, 2, 4, 8, 8, 16, 8, 8, 16, 8, 16, 16, 32, 32,

@@ -1,0 +1,60 @@
+// kernel_table.hpp -- the (op, element class) kernel tables of the C-ABI shim.
+//
+// g_table[op][elem].fn : the single-operand MPIR_Reduce_local launcher
+//                        (k_reduce_tile / k_reduce_shift / k_reduce_elems, or the
+//                        32-byte LDS-transpose kernel);
+// g_table[op][elem].any: the one-pass n-operand combine (k_combine_any), the
+//                        general path of MPIR_Hip_combine; REPLACE has none;
+// g_multi[op][elem][order][P = 2, 4, 8]: the fused schedule combines
+//                        (k_combine_multi) for the ops the collectives use most.
+// Storage lives in hip_reduce.hip (zero-initialised); the reg_*.hip units fill
+// it from static constructors, one unit per op family so they compile in
+// parallel.  The ops a type admits follow src/include/mpir_op_util.h:263-364.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "mpir_hip_reduce.h"
+#include "reduce_kernels.hpp"
+
+namespace mpir_hip {
+
+typedef hipError_t (*launch_fn)(const void *, void *, uint64_t, hipStream_t);
+typedef hipError_t (*any_fn)(const void *const *, int, int, void *, uint64_t, hipStream_t);
+typedef hipError_t (*multi_fn)(const void *const *, void *, uint64_t, hipStream_t);
+
+struct Entry { launch_fn fn; any_fn any; };
+extern Entry g_table[MPIR_HIP_NOPS][MPIR_HIP_NELEMS];
+extern multi_fn g_multi[MPIR_HIP_NOPS][MPIR_HIP_NELEMS][2][3];
+
+template <class Op, class T>
+void reg(int op, int elem) {
+    g_table[op][elem].fn = &launch_reduce<Op, T>;
+    if constexpr (!__is_same(Op, OpReplace)) g_table[op][elem].any = &launch_combine_any<Op, T>;
+}
+template <class Op, class T, int EPL = 2>
+void reg_wide(int op, int elem) {
+    g_table[op][elem].fn = &launch_reduce_wide<Op, T, EPL>;
+    g_table[op][elem].any = &launch_combine_any<Op, T>;
+}
+template <class Op, class T>
+void reg_multi(int op, int elem) {
+    g_multi[op][elem][0][0] = &launch_combine_p<Op, T, 2, true>;
+    g_multi[op][elem][0][1] = &launch_combine_p<Op, T, 4, true>;
+    g_multi[op][elem][0][2] = &launch_combine_p<Op, T, 8, true>;
+    g_multi[op][elem][1][0] = &launch_combine_p<Op, T, 2, false>;
+    g_multi[op][elem][1][1] = &launch_combine_p<Op, T, 4, false>;
+    g_multi[op][elem][1][2] = &launch_combine_p<Op, T, 8, false>;
+}
+
+}  // namespace mpir_hip
+
+// Integer element classes and their device types.
+#define FOR_INTS(X) \
+    X(MPIR_HIP_I8, int8_t) X(MPIR_HIP_U8, uint8_t) X(MPIR_HIP_I16, int16_t) X(MPIR_HIP_U16, uint16_t) \
+    X(MPIR_HIP_I32, int32_t) X(MPIR_HIP_U32, uint32_t) X(MPIR_HIP_I64, int64_t) X(MPIR_HIP_U64, uint64_t)
+#define FOR_REALS(X) X(MPIR_HIP_F16, f16) X(MPIR_HIP_F32, float) X(MPIR_HIP_F64, double)
+#define FOR_CPLX(X) X(MPIR_HIP_CF32, cf32) X(MPIR_HIP_CF64, cf64)
+#define FOR_PAIRS(X) \
+    X(MPIR_HIP_P2INT, p2int) X(MPIR_HIP_PFLOATINT, pfloatint) X(MPIR_HIP_PLONGINT, plongint) \
+    X(MPIR_HIP_PSHORTINT, pshortint) X(MPIR_HIP_PDOUBLEINT, pdoubleint)

@@ -511,7 +511,7 @@ static int reduce_scatter_short(struct MPIX_Hip_comm_s *c, const char *src, void
     return fold_tree(ys, pof2, recvbuf, rcount, opidx, elem, s, fc);
 }
 
-/* validation shared by both collectives (MPIR_ERRTEST_OP + check_dtype) */
+/* validation shared by the collectives (MPIR_ERRTEST_OP + check_dtype) */
 static int coll_check(const char *fc, const void *sendbuf, void *recvbuf, int count, MPI_Datatype dt, MPI_Op op,
                       MPIX_Hip_comm comm, int *elem)
 {
