@@ -45,6 +45,7 @@ MIB = 1 << 20
 GIB = 1 << 30
 HBM_PEAK_BPS = 8.0e12          # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 METRIC = "GiB/s device-resident MPI_Reduce_local (fp32 SUM, 256 MiB) at 1/2/4/8 GPUs"
+NPAIRS = 4                     # operand pairs rotated through (>= 3)
 
 
 def parse():
@@ -124,7 +125,7 @@ def config3_sweep(m, lib, pairs, nbytes: int, stream, k: int = 15, w: int = 5):
     """BASELINE config 3: {SUM, MAX, MIN, PROD} x {int32, int64, fp32, fp64} at 256 MiB
     per operand, kernel roofline fraction per (op, type).  The resident pairs are
     reinterpreted per type; PROD multiplies by an all-ones inbuf so repeated
-    in-place calls stay finite; two such buffers alternate like the
+    in-place calls stay finite; NPAIRS such buffers rotate like the
     pairs, so no launch re-reads what the previous one left in the Infinity Cache."""
     import torch
     types = [("int32", m.MPI_INT32_T, torch.int32), ("int64", m.MPI_INT64_T, torch.int64),
@@ -134,11 +135,11 @@ def config3_sweep(m, lib, pairs, nbytes: int, stream, k: int = 15, w: int = 5):
     for tname, dt, tt in types:
         esz = torch.tensor([], dtype=tt).element_size()
         count = nbytes // esz
-        ones = [torch.ones(count, dtype=tt, device="cuda") for _ in range(2)]
+        ones = [torch.ones(count, dtype=tt, device="cuda") for _ in range(NPAIRS)]
         for oname, op in ops:
             def launch(i):
-                a, b = pairs[i & 1]
-                pin = ones[i & 1].data_ptr() if oname == "PROD" else b.data_ptr()
+                a, b = pairs[i % NPAIRS]
+                pin = ones[i % NPAIRS].data_ptr() if oname == "PROD" else b.data_ptr()
                 rc = lib.MPIX_Reduce_local_stream(pin, a.data_ptr(), count, dt, op, stream.cuda_stream)
                 assert rc == 0, m.error_string(rc)
             with torch.cuda.stream(stream):
@@ -151,8 +152,8 @@ def config3_sweep(m, lib, pairs, nbytes: int, stream, k: int = 15, w: int = 5):
 
 
 def config2(m, lib, pairs, stream, k: int, w: int):
-    """BASELINE config 2: fp32 SUM, 64 MiB per operand.  Eight distinct 64 MiB
-    (inbuf, inoutbuf) windows of the resident buffers are rotated, 512 MiB of
+    """BASELINE config 2: fp32 SUM, 64 MiB per operand.  4 * NPAIRS distinct 64 MiB
+    (inbuf, inoutbuf) windows of the resident buffers are rotated, 2 GiB of
     footprint per cycle, so no call finds its operands in the 256 MB Infinity Cache."""
     import torch
     count = 16 * MIB
@@ -221,15 +222,15 @@ def main():
     count = nbytes // 4
     alg_bytes = 3 * nbytes
     g = torch.Generator(device="cuda").manual_seed(0x5EED + rank)
-    # two resident pairs, alternated, so consecutive steps never hit the
-    # Infinity Cache lines the previous step left behind
+    # NPAIRS resident pairs, rotated, so no step finds its operands in the
+    # 256 MB Infinity Cache (>= 3 pairs)
     pairs = [((torch.rand(count, device="cuda", generator=g) * 2 - 1),
-              (torch.rand(count, device="cuda", generator=g) * 2 - 1)) for _ in range(2)]
+              (torch.rand(count, device="cuda", generator=g) * 2 - 1)) for _ in range(NPAIRS)]
     ptrs = [(a.data_ptr(), b.data_ptr()) for a, b in pairs]
     sync()
 
     def step(i):
-        pin, pio = ptrs[i & 1]
+        pin, pio = ptrs[i % NPAIRS]
         rc = lib.MPI_Reduce_local(pin, pio, count, m.MPI_FLOAT, m.MPI_SUM)
         if rc:
             raise RuntimeError(m.error_string(rc))
@@ -270,10 +271,10 @@ def main():
                for _ in range(args.steps)]
         with torch.cuda.stream(s):
             for i in range(args.warmup):
-                pin, pio = ptrs[i & 1]
+                pin, pio = ptrs[i % NPAIRS]
                 lib.MPIX_Reduce_local_stream(pin, pio, count, m.MPI_FLOAT, m.MPI_SUM, s.cuda_stream)
             for i, (e0, e1) in enumerate(evs):
-                pin, pio = ptrs[i & 1]
+                pin, pio = ptrs[i % NPAIRS]
                 e0.record(s)
                 rc = lib.MPIX_Reduce_local_stream(pin, pio, count, m.MPI_FLOAT, m.MPI_SUM, s.cuda_stream)
                 e1.record(s)
@@ -305,7 +306,7 @@ def main():
 
         # ---- stream-ordered API, back to back (what the library's schedules drive)
         def sstep(i):
-            pin, pio = ptrs[i & 1]
+            pin, pio = ptrs[i % NPAIRS]
             lib.MPIX_Reduce_local_stream(pin, pio, count, m.MPI_FLOAT, m.MPI_SUM, None)
         dts = time_steps(sstep, args.steps, args.warmup, sync, barrier, max_over_ranks)
         out["stream_api"] = {"value": round(alg_bytes * args.steps * world / dts / GIB, 1), "unit": "GiB/s",
