@@ -136,6 +136,7 @@ def config3_sweep(m, lib, pairs, nbytes: int, stream, k: int = 15, w: int = 5):
         esz = torch.tensor([], dtype=tt).element_size()
         count = nbytes // esz
         ones = [torch.ones(count, dtype=tt, device="cuda") for _ in range(NPAIRS)]
+        torch.cuda.synchronize()    # the fills run on torch's stream, the timing on `stream`
         for oname, op in ops:
             def launch(i):
                 a, b = pairs[i % NPAIRS]
