@@ -371,6 +371,42 @@ static void cnts_disps(long count, int pof2, long *cnts, long *disps)
         disps[i] = disps[i - 1] + cnts[i - 1];
 }
 
+/* MPIR_Allreduce_intra_auto's branch (allreduce.c:145-217) from the CVARs a
+ * user can set (defaults in brackets): MPIR_CVAR_ENABLE_SMP_COLLECTIVES [1],
+ * MPIR_CVAR_ENABLE_SMP_ALLREDUCE [1], MPIR_CVAR_MAX_SMP_ALLREDUCE_MSG_SIZE [0],
+ * MPIR_CVAR_ALLREDUCE_SHORT_MSG_SIZE [2048].  The device communicator is taken
+ * as node-aware (one node).  Note the reference's nbytes: it is 0 unless
+ * MAX_SMP_ALLREDUCE_MSG_SIZE is set (:159), so the flat branch then always picks
+ * recursive doubling. */
+#define FLAT_NO 0
+#define FLAT_RECURSIVE_DOUBLING 1
+#define FLAT_RABENSEIFNER 2
+static long cvar_long(const char *name, long dflt)
+{
+    const char *v = getenv(name);
+    return v && *v ? strtol(v, NULL, 0) : dflt;
+}
+
+static int allreduce_flat_choice(size_t bytes, long count, int pof2)
+{
+    const long max_smp = cvar_long("MPIR_CVAR_MAX_SMP_ALLREDUCE_MSG_SIZE", 0);
+    const long nbytes = max_smp ? (long) bytes : 0;
+    if (cvar_long("MPIR_CVAR_ENABLE_SMP_COLLECTIVES", 1) && cvar_long("MPIR_CVAR_ENABLE_SMP_ALLREDUCE", 1) &&
+        nbytes <= max_smp)
+        return FLAT_NO;
+    if (nbytes <= cvar_long("MPIR_CVAR_ALLREDUCE_SHORT_MSG_SIZE", 2048) || count < pof2)
+        return FLAT_RECURSIVE_DOUBLING;
+    return FLAT_RABENSEIFNER;
+}
+
+/* real rank of newrank m after the pre-fold: the keeper of pair m is the even
+ * rank 2m (reduce_intra_reduce_scatter_gather.c) or the odd rank 2m+1
+ * (allreduce_intra_reduce_scatter_allgather.c, allreduce_intra_recursive_doubling.c) */
+static int real_of(int m, int rem, int odd_keeps)
+{
+    return m < rem ? 2 * m + (odd_keeps ? 1 : 0) : m + rem;
+}
+
 /* ------------------------------------------------------------ short messages
  * MPICH switches algorithm on message size.  For these the device form keeps
  * the reference's association and operand order but not its rounds: ONE
@@ -451,6 +487,52 @@ static int allreduce_short(struct MPIX_Hip_comm_s *c, const void *sendbuf, void 
                 return rc;
     e = hipMemcpyAsync(recvbuf, scr, bytes, hipMemcpyDeviceToDevice, s);
     return e == hipSuccess ? MPI_SUCCESS : hip_err(fc, e);
+}
+
+/* MPI_Allreduce, flat branch, recursive doubling
+ * (allreduce_intra_recursive_doubling.c): even r < 2*rem sends to r+1, which
+ * computes Y = x_{r} (+) x_{r-1}; then at mask 1, 2, 4, ... newrank n folds in
+ * the partial of n ^ mask second, so n ends with the tree over z_j = Y_{n ^ j};
+ * an excluded even rank receives the result of its odd neighbour.  Here: an
+ * allgather of the p inputs, the rem pre-fold steps, one tree combine per rank. */
+static int allreduce_recursive_doubling(struct MPIX_Hip_comm_s *c, const void *sendbuf, void *recvbuf,
+                                        long count, size_t esz, int opidx, int elem, hipStream_t s,
+                                        const char *fc)
+{
+    int p = c->size, q, nx = 0, rc = MPI_SUCCESS, pof2 = pof2_of(p), rem = p - pof2, n, j, m;
+    size_t bytes = (size_t) count * esz, slot = (bytes + 255) & ~(size_t) 255;
+    xfer_t sends[MAX_XFER], recvs[MAX_XFER];
+    const void *ys[64];
+    char *scr = NULL, *own;
+    hipError_t e;
+    if (comm_scratch(c, (size_t) p * slot, &scr)) {
+        MPIR_Err_set_detail("%s: scratch allocation failed", fc);
+        return MPI_ERR_NO_MEM;
+    }
+    own = scr + (size_t) c->rank * slot;
+    e = hipMemcpyAsync(own, sendbuf == MPI_IN_PLACE ? recvbuf : sendbuf, bytes, hipMemcpyDeviceToDevice, s);
+    if (e != hipSuccess)
+        return hip_err(fc, e);
+    for (q = 0; q < p; q++) {
+        if (q == c->rank)
+            continue;
+        sends[nx].buf = own;
+        sends[nx].bytes = bytes;
+        sends[nx].peer = q;
+        recvs[nx].buf = scr + (size_t) q * slot;
+        recvs[nx].bytes = bytes;
+        recvs[nx++].peer = q;
+    }
+    if ((rc = group_exchange(c, sends, nx, recvs, nx, s)) != MPI_SUCCESS)
+        return rc;
+    for (m = 0; m < rem; m++)
+        if ((rc = fold_step(scr + (size_t) (2 * m) * slot, scr + (size_t) (2 * m + 1) * slot, count, opidx,
+                            elem, s, fc)) != MPI_SUCCESS)
+            return rc;
+    n = c->rank < 2 * rem ? c->rank / 2 : c->rank - rem;
+    for (j = 0; j < pof2; j++)
+        ys[j] = scr + (size_t) real_of(n ^ j, rem, 1) * slot;
+    return fold_tree(ys, pof2, recvbuf, count, opidx, elem, s, fc);
 }
 
 /* MPI_Reduce_scatter(_block), total bytes < 524288: recursive halving
@@ -587,27 +669,31 @@ static int want_rccl(struct MPIX_Hip_comm_s *c, int algorithm, int elem, int opi
  * ((y0+y1)+(y2+y3))+... with y_j = the block from newrank n ^ j.
  * `scr` holds (pof2-1) * cnts[0] elements + count elements + 256 bytes.
  * Returns this rank's newrank in *newrank (-1: excluded by the pre-fold). */
+
 static int rsg_phase(struct MPIX_Hip_comm_s *c, char *work, long count, size_t esz, int opidx, int elem,
-                     hipStream_t s, const char *fc, char *scr, const long *cnts, const long *disps, int *newrank)
+                     hipStream_t s, const char *fc, char *scr, const long *cnts, const long *disps, int odd_keeps,
+                     int *newrank)
 {
     int p = c->size, pof2 = pof2_of(p), rem = p - pof2, bits = 0, nsend = 0, nrecv = 0, rc, i;
     size_t bytes = (size_t) count * esz, maxblk = (size_t) cnts[0];
     xfer_t sends[MAX_XFER], recvs[MAX_XFER];
     while ((1 << bits) < pof2)
         bits++;
-    /* pre-fold; every rank takes part in the transfer group (empty for ranks >= 2*rem) */
+    /* pre-fold; every rank takes part in the transfer group (empty for ranks >= 2*rem).
+     * The keeper folds its partner's vector in as the second operand. */
     if (rem > 0 && c->rank >= 2 * rem)
         if ((rc = group_exchange(c, NULL, 0, NULL, 0, s)) != MPI_SUCCESS)
             return rc;
     if (c->rank < 2 * rem) {
-        if (c->rank % 2) {
-            xfer_t x = { work, bytes, c->rank - 1 };
+        const int keeper = (c->rank % 2) == (odd_keeps ? 1 : 0);
+        if (!keeper) {
+            xfer_t x = { work, bytes, odd_keeps ? c->rank + 1 : c->rank - 1 };
             if ((rc = group_exchange(c, &x, 1, NULL, 0, s)) != MPI_SUCCESS)
                 return rc;
             *newrank = -1;
         } else {
             char *tmp = scr + (size_t) (pof2 > 1 ? pof2 - 1 : 1) * maxblk * esz;
-            xfer_t x = { tmp, bytes, c->rank + 1 };
+            xfer_t x = { tmp, bytes, odd_keeps ? c->rank - 1 : c->rank + 1 };
             if ((rc = group_exchange(c, NULL, 0, &x, 1, s)) != MPI_SUCCESS)
                 return rc;
             if ((rc = fold_step(tmp, work, count, opidx, elem, s, fc)) != MPI_SUCCESS)
@@ -625,7 +711,7 @@ static int rsg_phase(struct MPIX_Hip_comm_s *c, char *work, long count, size_t e
             int real, b;
             if (m == n)
                 continue;
-            real = m < rem ? 2 * m : m + rem;
+            real = real_of(m, rem, odd_keeps);
             b = bitrev(m, bits);
             sends[nsend].buf = work + disps[b] * esz;
             sends[nsend].bytes = (size_t) cnts[b] * esz;
@@ -655,7 +741,7 @@ int MPIX_Allreduce_hip(const void *sendbuf, void *recvbuf, int count, MPI_Dataty
 {
     static const char *fc = "MPIX_Allreduce_hip";
     struct MPIX_Hip_comm_s *c = comm;
-    int elem = 0, opidx = op & 0xf, rc, p, pof2, rem, newrank = -1, bits, i;
+    int elem = 0, opidx = op & 0xf, rc, p, pof2, rem, newrank = -1, bits, i, flat, odd_keeps;
     size_t esz, bytes;
     hipStream_t s;
     ncclDataType_t nt;
@@ -687,18 +773,28 @@ int MPIX_Allreduce_hip(const void *sendbuf, void *recvbuf, int count, MPI_Dataty
         goto done_sync;
     }
 
-    /* ---- reference order (allreduce_intra_smp.c + MPIR_Reduce_intra_auto's choice) */
+    /* ---- reference order: MPIR_Allreduce_intra_auto (allreduce.c:145-217).  On one
+     * node the SMP branch runs (allreduce_intra_smp.c: MPIR_Reduce with
+     * MPIR_Reduce_intra_auto's choice, then MPIR_Bcast); with the SMP CVARs off
+     * (or a comm with one rank per node) the flat branch runs */
     pof2 = pof2_of(p);
     if (p == 1) {
         if (sendbuf != MPI_IN_PLACE)
             HIPTRY(hipMemcpyAsync(recvbuf, sendbuf, bytes, hipMemcpyDeviceToDevice, s));
         goto done_sync;
     }
-    if (bytes <= REDUCE_SHORT_MSG_SIZE || count < pof2) {
+    flat = allreduce_flat_choice(bytes, count, pof2);
+    if (flat == FLAT_RECURSIVE_DOUBLING) {
+        TRY(allreduce_recursive_doubling(c, sendbuf, recvbuf, count, esz, opidx, elem, s, fc));
+        goto done_sync;
+    }
+    odd_keeps = flat == FLAT_RABENSEIFNER;
+    if (!flat && (bytes <= REDUCE_SHORT_MSG_SIZE || count < pof2)) {
         TRY(allreduce_short(c, sendbuf, recvbuf, count, esz, opidx, elem, s, fc));
         goto done_sync;
     }
-    /* long: reduce_intra_reduce_scatter_gather.c's reduce-scatter on recvbuf */
+    /* long: the reduce-scatter of reduce_intra_reduce_scatter_gather.c (SMP) or
+     * allreduce_intra_reduce_scatter_allgather.c (flat, Rabenseifner) on recvbuf */
     if (sendbuf != MPI_IN_PLACE)
         HIPTRY(hipMemcpyAsync(recvbuf, sendbuf, bytes, hipMemcpyDeviceToDevice, s));
     rem = p - pof2;
@@ -711,7 +807,7 @@ int MPIX_Allreduce_hip(const void *sendbuf, void *recvbuf, int count, MPI_Dataty
         rc = MPI_ERR_NO_MEM;
         goto done;
     }
-    TRY(rsg_phase(c, recvbuf, count, esz, opidx, elem, s, fc, scr, cnts, disps, &newrank));
+    TRY(rsg_phase(c, recvbuf, count, esz, opidx, elem, s, fc, scr, cnts, disps, odd_keeps, &newrank));
 
     /* allgather of the reduced blocks to every rank (the gather + MPIR_Bcast of
      * allreduce_intra_smp.c move data only) */
@@ -727,7 +823,7 @@ int MPIX_Allreduce_hip(const void *sendbuf, void *recvbuf, int count, MPI_Dataty
         }
     }
     for (i = 0; i < pof2; i++) {
-        int real = i < rem ? 2 * i : i + rem, b = bitrev(i, bits);
+        int real = real_of(i, rem, odd_keeps), b = bitrev(i, bits);
         if (real == c->rank)
             continue;
         recvs[nrecv].buf = (char *) recvbuf + disps[b] * esz;
@@ -858,7 +954,7 @@ int MPIX_Reduce_hip(const void *sendbuf, void *recvbuf, int count, MPI_Datatype 
     work = isroot ? (char *) recvbuf : scr + slot;
     if (work != own)
         HIPTRY(hipMemcpyAsync(work, own, bytes, hipMemcpyDeviceToDevice, s));
-    TRY(rsg_phase(c, work, count, esz, opidx, elem, s, fc, scr, cnts, disps, &newrank));
+    TRY(rsg_phase(c, work, count, esz, opidx, elem, s, fc, scr, cnts, disps, 0, &newrank));
 
     /* gather of the owners' blocks to the root (reduce_intra_reduce_scatter_gather.c:256-410) */
     if (newrank >= 0 && !isroot) {
@@ -869,7 +965,7 @@ int MPIX_Reduce_hip(const void *sendbuf, void *recvbuf, int count, MPI_Datatype 
     }
     if (isroot) {
         for (i = 0; i < pof2; i++) {
-            int real = i < rem ? 2 * i : i + rem, b = bitrev(i, bits);
+            int real = real_of(i, rem, 0), b = bitrev(i, bits);
             if (real == c->rank)
                 continue;
             recvs[nrecv].buf = (char *) recvbuf + disps[b] * esz;

@@ -380,3 +380,54 @@ def exscan_recursive_doubling(rank_sendbufs: list[np.ndarray], count: int, esz: 
                               op: int) -> list[np.ndarray]:
     """MPI_Exscan (MPIR_Exscan_intra_auto -> recursive doubling); rank 0 -> None."""
     return _scan_rd(rank_sendbufs, count, dt, op, exclusive=True)
+
+
+def allreduce_recursive_doubling(rank_bufs: list[np.ndarray], count: int, esz: int, dt: int,
+                                 op: int) -> list[np.ndarray]:
+    """MPI_Allreduce's flat-branch recursive doubling, step by step
+    (allreduce_intra_recursive_doubling.c): even r < 2*rem sends to r+1, which
+    folds it in second (x_r (+) x_{r-1}); then at mask 1, 2, 4, ... every newrank
+    exchanges its accumulation with newrank ^ mask and folds the received one in
+    second; odd r < 2*rem finally hands its result to r-1.  Per-rank results
+    (they can differ in operand order, e.g. MAX of +0 / -0)."""
+    p = len(rank_bufs)
+    pof2 = _pof2(p)
+    rem = p - pof2
+    acc = [b.view(np.uint8).reshape(-1).copy() for b in rank_bufs]
+    real = {}
+    for r in range(p):
+        if r < 2 * rem:
+            if r % 2:
+                _red(acc[r - 1].copy(), acc[r], count, dt, op)
+                real[r // 2] = r
+        else:
+            real[r - rem] = r
+    mask = 1
+    while mask < pof2:
+        sent = {r: acc[r].copy() for r in real.values()}
+        for n, r in real.items():
+            _red(sent[real[n ^ mask]].copy(), acc[r], count, dt, op)
+        mask <<= 1
+    for r in range(0, 2 * rem, 2):
+        acc[r] = acc[r + 1].copy()
+    return acc
+
+
+def allreduce_auto(rank_bufs: list[np.ndarray], count: int, esz: int, dt: int, op: int, smp: bool = True,
+                   max_smp: int = 0, short: int = 2048) -> list[np.ndarray]:
+    """MPIR_Allreduce_intra_auto (allreduce.c:145-217) for a builtin op on one node,
+    per rank.  nbytes is 0 unless MPIR_CVAR_MAX_SMP_ALLREDUCE_MSG_SIZE is set
+    (:159), so the SMP branch is taken whenever the SMP CVARs are on, and the flat
+    branch then picks recursive doubling; Rabenseifner needs max_smp > 0 and a
+    message above `short` with count >= pof2."""
+    p = len(rank_bufs)
+    nbytes = count * esz if max_smp else 0
+    if smp and nbytes <= max_smp:
+        res = allreduce_smp_auto(rank_bufs, count, esz, dt, op)
+        return [res.copy() for _ in range(p)]
+    if p == 1:
+        return [rank_bufs[0].view(np.uint8).reshape(-1).copy()]
+    if nbytes <= short or count < _pof2(p):
+        return allreduce_recursive_doubling(rank_bufs, count, esz, dt, op)
+    res = allreduce_rsag(rank_bufs, count, esz, dt, op)
+    return [res.copy() for _ in range(p)]

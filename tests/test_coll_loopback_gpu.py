@@ -301,6 +301,47 @@ def test_scan_reference_order(mpi, orc, cuda, t, op, p, inplace, exclusive):
             mpi.comm_free(c)
 
 
+FLAT = [("MPI_FLOAT", "MPI_SUM"), ("MPI_DOUBLE", "MPI_MAX"), ("MPIX_C_FLOAT16", "MPI_SUM"), ("MPI_2INT", "MPI_MAXLOC")]
+
+
+@pytest.mark.parametrize("t,op", FLAT, ids=[f"{t}-{o}" for t, o in FLAT])
+@pytest.mark.parametrize("p", [2, 3, 5, 8])
+@pytest.mark.parametrize("cvars", ["smp_off", "max_smp_1"])
+def test_allreduce_flat_branch(mpi, orc, cuda, t, op, p, cvars, monkeypatch):
+    """MPIR_Allreduce_intra_auto's flat branch, selected by the reference's CVARs:
+    MPIR_CVAR_ENABLE_SMP_COLLECTIVES=0 (recursive doubling at every size: nbytes
+    is 0 while MAX_SMP_ALLREDUCE_MSG_SIZE is 0) and
+    MPIR_CVAR_MAX_SMP_ALLREDUCE_MSG_SIZE=1 (recursive doubling short,
+    Rabenseifner long).  Per-rank results vs the step-by-step schedules."""
+    from oracle import schedules as S
+    torch = cuda
+    esz = T.elem_size(t)
+    dt, o = mpi.DATATYPES[t], mpi.OPS[op]
+    if cvars == "smp_off":
+        monkeypatch.setenv("MPIR_CVAR_ENABLE_SMP_COLLECTIVES", "0")
+        kw = dict(smp=False)
+    else:
+        monkeypatch.setenv("MPIR_CVAR_MAX_SMP_ALLREDUCE_MSG_SIZE", "1")
+        kw = dict(smp=True, max_smp=1)
+    comms = mpi.comm_create_loopback(p)
+    try:
+        for count, seed in ((3, p), (2048 // esz + 1, 2 * p), ((1 << 17) + 7, 3 * p)):
+            rng = np.random.default_rng(seed)
+            xs = [T.to_bytes(T.gen(t, count, rng, op)) for _ in range(p)]
+            want = S.allreduce_auto(xs, count, esz, dt, o, **kw)
+            send = [torch.from_numpy(x.copy()).cuda() for x in xs]
+            recv = [torch.zeros_like(x) for x in send]
+            torch.cuda.synchronize()
+            run_ranks(lambda r: _ok(mpi, mpi.allreduce(send[r].data_ptr(), recv[r].data_ptr(), count, dt, o,
+                                                       comms[r], mpi.MPIX_HIP_ALG_REFERENCE_ORDER)), p)
+            torch.cuda.synchronize()
+            for r in range(p):
+                assert same(recv[r].cpu().numpy(), want[r], t), f"count {count} rank {r}"
+    finally:
+        for c in comms:
+            mpi.comm_free(c)
+
+
 def test_reduce_validation(mpi, cuda):
     torch = cuda
     comms = mpi.comm_create_loopback(2)

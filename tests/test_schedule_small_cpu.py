@@ -219,3 +219,41 @@ def test_scan_plan(orc, t, op, p, exclusive):
         for x in chain[1:]:
             _red(orc, x, acc, count, t, op)
         assert np.array_equal(acc, want[r]), f"rank {r}"
+
+
+@pytest.mark.parametrize("t,op", CASES)
+@pytest.mark.parametrize("p", [2, 3, 5, 6, 8, 11])
+def test_allreduce_flat_recursive_doubling_plan(orc, t, op, p):
+    """Flat-branch Allreduce (SMP CVARs off): rank r's result is the tree over
+    z_j = Y_{n ^ j}, Y_m = x_{2m+1} (+) x_{2m} for m < rem, n = r's newrank
+    (an excluded even rank takes its odd neighbour's)."""
+    from oracle import schedules as S
+    esz = T.elem_size(t)
+    count = 9
+    xs = _inputs(t, op, count, p, 13 * p)
+    want = S.allreduce_auto(xs, count, esz, DATATYPES[t], OPS[op], smp=False)
+    pof2 = _pof2(p)
+    rem = p - pof2
+    for r in range(p):
+        slots = [x.copy() for x in xs]
+        for m in range(rem):
+            _red(orc, slots[2 * m], slots[2 * m + 1], count, t, op)
+        n = r // 2 if r < 2 * rem else r - rem
+        real = [2 * m + 1 if m < rem else m + rem for m in range(pof2)]
+        got = tree_fold(orc, [slots[real[n ^ j]] for j in range(pof2)], count, t, op)
+        assert np.array_equal(got, want[r]), f"rank {r}"
+
+
+def test_allreduce_flat_branch_choice(orc):
+    """nbytes is 0 unless MAX_SMP_ALLREDUCE_MSG_SIZE is set: with the SMP CVARs
+    off the flat branch is recursive doubling at every size; Rabenseifner only
+    with a nonzero MAX_SMP_ALLREDUCE_MSG_SIZE and a long message."""
+    from oracle import schedules as S
+    p, count = 6, 4099
+    xs = _inputs("MPI_DOUBLE", "MPI_SUM", count, p, 1)
+    dt, o = DATATYPES["MPI_DOUBLE"], OPS["MPI_SUM"]
+    rd = S.allreduce_recursive_doubling(xs, count, 8, dt, o)
+    assert all(np.array_equal(a, b) for a, b in zip(S.allreduce_auto(xs, count, 8, dt, o, smp=False), rd))
+    rab = S.allreduce_rsag(xs, count, 8, dt, o)
+    got = S.allreduce_auto(xs, count, 8, dt, o, smp=True, max_smp=1)
+    assert all(np.array_equal(a, rab) for a in got)
