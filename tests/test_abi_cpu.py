@@ -202,3 +202,18 @@ def test_error_class_and_string(mpi):
     c = ctypes.c_int(-1)
     assert lib.MPI_Error_class(mpi.MPI_ERR_OP, ctypes.byref(c)) == 0 and c.value == mpi.MPI_ERR_OP
     assert mpi.error_string(0) == "No MPI error"
+
+
+@pytest.mark.parametrize("compiler", [["gcc", "-std=c99", "-pedantic"], ["g++", "-std=c++17", "-x", "c++"]],
+                         ids=["c99", "c++17"])
+def test_public_headers_compile_and_link(mpi, tmp_path, compiler):
+    """include/*.h are self-contained C99 and C++; the entry points have the
+    reference prototypes; a program using them links against the library."""
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    lib = os.path.join(root, "mpich-pip_amd", "lib")
+    exe = str(tmp_path / "abi_link")
+    subprocess.run([*compiler, "-Wall", "-Wextra", "-Werror", "-I" + os.path.join(root, "include"),
+                    os.path.join(root, "tests", "progs", "abi_link.c"), "-o", exe, "-L" + lib,
+                    "-lmpich_reduce_local", "-Wl,-rpath," + lib], check=True)
+    assert subprocess.run([exe]).returncode == 0
