@@ -93,6 +93,10 @@ int MPIR_Hip_memcpy(void *dst, const void *src, size_t bytes);
 const char *MPIR_Hip_error_string(void);
 /* number of visible devices (0 if none / runtime unavailable) */
 int MPIR_Hip_device_count(void);
+/* per-thread contexts (streams, completion word, scratch) created so far; a
+   context returns to a pool when its thread exits and is reused, so this stays
+   at the peak number of threads calling at once (diagnostic) */
+int MPIR_Hip_thread_contexts(void);
 
 #ifdef __cplusplus
 }

@@ -10,6 +10,8 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <mutex>
+
 #include "mpir_hip_reduce.h"
 #include "kernel_table.hpp"
 
@@ -78,19 +80,58 @@ struct DevCtx {
 struct ThreadCtx {
     DevCtx dev[kMaxDev];
     char err[256] = {0};
+    ThreadCtx *next = nullptr;
 };
 
-thread_local ThreadCtx t_ctx;
+// Per-thread contexts (streams, events, completion word, scratch) come from a
+// process-wide pool: a thread takes one at its first call and hands it back
+// when it exits, so an application that starts and ends many threads reuses
+// a bounded set of HIP streams instead of leaking one set per thread.  A
+// handed-back context keeps its streams (work still queued on them stays in
+// order for the next owner); thread exit makes no HIP call, so it is safe at
+// process teardown too.
+std::mutex g_pool_mu;
+ThreadCtx *g_pool = nullptr;
+int g_ctx_created = 0;
+
+struct CtxHolder {
+    ThreadCtx *c = nullptr;
+    ThreadCtx &get() {
+        if (!c) {
+            std::lock_guard<std::mutex> lk(g_pool_mu);
+            if (g_pool) {
+                c = g_pool;
+                g_pool = c->next;
+                c->next = nullptr;
+                c->err[0] = 0;
+            } else {
+                c = new ThreadCtx();
+                ++g_ctx_created;
+            }
+        }
+        return *c;
+    }
+    ~CtxHolder() {
+        if (!c) return;
+        std::lock_guard<std::mutex> lk(g_pool_mu);
+        c->next = g_pool;
+        g_pool = c;
+        c = nullptr;
+    }
+};
+
+thread_local CtxHolder t_holder;
+inline ThreadCtx &ctx() { return t_holder.get(); }
 
 int set_err(hipError_t e, const char *what) {
-    snprintf(t_ctx.err, sizeof(t_ctx.err), "%s: %s", what, hipGetErrorString(e));
+    snprintf(ctx().err, sizeof(ctx().err), "%s: %s", what, hipGetErrorString(e));
     return MPIR_HIP_ERUNTIME;
 }
 
 #define HIPCHK(call) do { hipError_t e_ = (call); if (e_ != hipSuccess) return set_err(e_, #call); } while (0)
 
 int get_stream(int dev, int slot, hipStream_t *out) {
-    DevCtx &d = t_ctx.dev[dev];
+    DevCtx &d = ctx().dev[dev];
     if (!d.stream[slot]) {
         // Blocking stream (not hipStreamNonBlocking): it orders after work the
         // caller queued on the legacy null stream for these buffers.
@@ -101,7 +142,7 @@ int get_stream(int dev, int slot, hipStream_t *out) {
 }
 
 int get_stage_events(int dev, int nslots) {
-    DevCtx &d = t_ctx.dev[dev];
+    DevCtx &d = ctx().dev[dev];
     for (int k = 0; k < nslots; ++k) {
         if (!d.ev_up[k]) HIPCHK(hipEventCreateWithFlags(&d.ev_up[k], hipEventDisableTiming));
         if (!d.ev_comp[k]) HIPCHK(hipEventCreateWithFlags(&d.ev_comp[k], hipEventDisableTiming));
@@ -111,7 +152,7 @@ int get_stage_events(int dev, int nslots) {
 }
 
 int get_scratch(int dev, size_t bytes, char **out) {
-    DevCtx &d = t_ctx.dev[dev];
+    DevCtx &d = ctx().dev[dev];
     if (d.scratch_bytes < bytes) {
         // stream-ordered users of the old scratch may still be in flight
         if (d.scratch) HIPCHK(hipDeviceSynchronize());
@@ -169,7 +210,7 @@ int wait_stream_block(hipStream_t s) {
 
 int wait_stream(int dev, hipStream_t s) {
     if (wait_mode() == 0) return wait_stream_block(s);
-    DevCtx &d = t_ctx.dev[dev];
+    DevCtx &d = ctx().dev[dev];
     if (!d.flag) {
         void *p = nullptr;
         if (hipHostMalloc(&p, 64, hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess) {
@@ -207,7 +248,12 @@ int MPIR_Hip_has_kernel(int op, int elem) {
     return g_table[op][elem].fn != nullptr;
 }
 
-const char *MPIR_Hip_error_string(void) { return t_ctx.err; }
+const char *MPIR_Hip_error_string(void) { return ctx().err; }
+
+int MPIR_Hip_thread_contexts(void) {
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    return g_ctx_created;
+}
 
 int MPIR_Hip_device_count(void) {
     int n = 0;
@@ -228,7 +274,7 @@ int MPIR_Hip_memcpy(void *dst, const void *src, size_t bytes) {
 
 int MPIR_Hip_combine(const void *const *inbufs, int n, void *outbuf, uint64_t count, int op, int elem,
                      int order, void *hip_stream, int sync) {
-    t_ctx.err[0] = 0;
+    ctx().err[0] = 0;
     if (n < 1 || n > 64 || (order != MPIR_HIP_ORDER_TREE && order != MPIR_HIP_ORDER_CHAIN)) return MPIR_HIP_ENOKERNEL;
     if (op <= 0 || op >= MPIR_HIP_NOPS || elem <= 0 || elem >= MPIR_HIP_NELEMS) return MPIR_HIP_ENOKERNEL;
     if (order == MPIR_HIP_ORDER_TREE && (n & (n - 1))) return MPIR_HIP_ENOKERNEL;
@@ -286,7 +332,7 @@ int MPIR_Hip_combine(const void *const *inbufs, int n, void *outbuf, uint64_t co
 
 int MPIR_Hip_reduce(const void *inbuf, void *inoutbuf, uint64_t count, int op, int elem, void *hip_stream,
                     int sync) {
-    t_ctx.err[0] = 0;
+    ctx().err[0] = 0;
     if (!MPIR_Hip_has_kernel(op, elem)) return MPIR_HIP_ENOKERNEL;
     if (count == 0) return MPIR_HIP_OK;
     launch_fn fn = g_table[op][elem].fn;
@@ -331,7 +377,7 @@ int MPIR_Hip_reduce(const void *inbuf, void *inoutbuf, uint64_t count, int op, i
     if (cur != dev) HIPCHK(hipSetDevice(dev));
 
     int rc = MPIR_HIP_OK;
-    DevCtx &d = t_ctx.dev[dev];
+    DevCtx &d = ctx().dev[dev];
     const bool stage_in = !(lin == LOC_DEVICE && din == dev);
     const bool stage_io = !(lio == LOC_DEVICE && dio == dev);
     const uint64_t total = count * esz;

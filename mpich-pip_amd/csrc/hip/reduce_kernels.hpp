@@ -81,7 +81,7 @@ __device__ __forceinline__ u32x4 combine16(u32x4 a, u32x4 b) {
 }
 
 template <class Op, class T>
-__global__ __launch_bounds__(kThreads) void k_reduce_tile(TileArgs<T> args) {
+__device__ __forceinline__ void reduce_tile_body(const TileArgs<T> &args) {
     const uint64_t base = (uint64_t)blockIdx.x * kTileBytes;
     if (base < args.vbytes) {
         const uint64_t left = args.vbytes - base;
@@ -107,6 +107,11 @@ __global__ __launch_bounds__(kThreads) void k_reduce_tile(TileArgs<T> args) {
         if (t < args.nhead) args.head_io[t] = op(args.head_io[t], args.head_in[t]);
         else if (t >= 64 && t - 64 < args.ntail) args.tail_io[t - 64] = op(args.tail_io[t - 64], args.tail_in[t - 64]);
     }
+}
+
+template <class Op, class T>
+__global__ __launch_bounds__(kThreads) void k_reduce_tile(TileArgs<T> args) {
+    reduce_tile_body<Op, T>(args);
 }
 
 // inbuf misaligned relative to inoutbuf: (in - io) mod 16 = delta != 0, the

@@ -435,3 +435,34 @@ def test_concurrent_host_threads(mpi, orc, cuda):
     assert not errs
     for da, db, w in data:
         assert np.array_equal(da.cpu().numpy(), w)
+
+
+def test_thread_contexts_reused(mpi, cuda):
+    """Per-thread HIP contexts return to a pool at thread exit: 64 short-lived
+    threads, 4 alive at a time, create at most the peak concurrency's worth of
+    new contexts (streams, completion words), and every call stays exact."""
+    import threading
+    torch = cuda
+    n = 4099
+    x = torch.arange(n, dtype=torch.int64, device="cuda")
+    ones = torch.ones(n, dtype=torch.int64, device="cuda")
+    torch.cuda.synchronize()
+    assert mpi.reduce_local(ones.data_ptr(), x.data_ptr(), n, mpi.MPI_INT64_T, mpi.MPI_SUM) == 0
+    before = mpi.load().MPIR_Hip_thread_contexts()
+    lock = threading.Lock()
+    errs = []
+
+    def work():
+        with lock:
+            if mpi.reduce_local(ones.data_ptr(), x.data_ptr(), n, mpi.MPI_INT64_T, mpi.MPI_SUM):
+                errs.append(mpi.load().MPIR_Hip_error_string())
+
+    for _ in range(16):
+        ths = [threading.Thread(target=work) for _ in range(4)]
+        for t in ths:
+            t.start()
+        for t in ths:
+            t.join(60)
+    assert not errs
+    assert mpi.load().MPIR_Hip_thread_contexts() - before <= 4
+    assert torch.equal(x, torch.arange(n, dtype=torch.int64, device="cuda") + 65)
