@@ -166,6 +166,15 @@ def config2(m, lib, pairs, stream, k: int, w: int):
                                             stream.cuda_stream) == 0
     with torch.cuda.stream(stream):
         us = event_launch_us(launch, k, w, stream)
+        # back to back: one event pair around K launches (no event packets between
+        # launches, so one launch's ramp-up overlaps the previous one's drain)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for i in range(k):
+            launch(w + k + i)
+        e1.record(stream)
+    stream.synchronize()
+    us_b2b = e0.elapsed_time(e1) * 1e3 / k
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(k):
@@ -174,6 +183,7 @@ def config2(m, lib, pairs, stream, k: int, w: int):
     dt = time.perf_counter() - t0
     alg = 3 * count * 4
     return {"kernel_us": round(us, 2), "kernel_frac": round(alg / (us * 1e-6) / HBM_PEAK_BPS, 4),
+            "back_to_back_us": round(us_b2b, 2), "back_to_back_frac": round(alg / (us_b2b * 1e-6) / HBM_PEAK_BPS, 4),
             "sync_api_GiBps": round(alg * k / dt / GIB, 1), "windows": len(wins)}
 
 

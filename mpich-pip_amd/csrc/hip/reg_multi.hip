@@ -1,7 +1,9 @@
 // reg_multi.hip -- fused schedule combines (k_combine_multi) for the ops the
 // reduction collectives are built on (configs 4-5): SUM / PROD / MAX / MIN over
-// the 32/64-bit integers and the reals, plus complex SUM.  Every other pair
-// takes k_combine_any (one pass, any n) through MPIR_Hip_combine.
+// the 32/64-bit integers and the reals, plus complex SUM.  reg_multi_small /
+// _logic / _bits.hip register every other pair of 16 bytes or less; the 32-byte
+// types (long double _Complex, MPI_LONG_DOUBLE_INT) and TREE folds of n > 8
+// take k_combine_any (one pass, any n) through MPIR_Hip_combine.
 #include "kernel_table.hpp"
 
 using namespace mpir_hip;

@@ -279,6 +279,38 @@ def test_user_op_on_device_buffers(mpi, cuda):
     assert lib.MPI_Op_free(ctypes.byref(op)) == 0
 
 
+def test_reference_reduce_local_program(mpi, cuda):
+    """The reference's own MPI_Reduce_local test (test/mpi/coll/reduce_local.c:
+    MPI_INT with MPI_SUM, then a non-commutative user op, counts 0, 1, 2, 4, ...,
+    32768, inbuf[i] = inoutbuf[i] = i) on device buffers.  Its result check is
+    nested inside the inbuf check (reduce_local.c:63-65, 80-82), so
+    here both buffers are checked: inbuf unchanged, inoutbuf = 2i for SUM and
+    the user op's value for every element."""
+    torch = cuda
+    lib = mpi.load()
+
+    @mpi.MPI_User_function
+    def user_op(invec, inoutvec, lenp, dtp):
+        n = lenp[0]
+        a = np.ctypeslib.as_array(ctypes.cast(invec, ctypes.POINTER(ctypes.c_int)), (n,))
+        b = np.ctypeslib.as_array(ctypes.cast(inoutvec, ctypes.POINTER(ctypes.c_int)), (n,))
+        b[:] = a - 3 * b          # non-commutative: f(a, b) != f(b, a)
+
+    uop = ctypes.c_int(0)
+    assert lib.MPI_Op_create(user_op, 0, ctypes.byref(uop)) == 0
+    counts = [0] + [1 << k for k in range(16)]
+    for count in counts:
+        ref = torch.arange(count, dtype=torch.int32, device="cuda")
+        for op, want in ((mpi.MPI_SUM, 2 * ref), (uop.value, ref - 3 * ref)):
+            inb = ref.clone()
+            io = ref.clone()
+            torch.cuda.synchronize()
+            assert mpi.reduce_local(inb.data_ptr(), io.data_ptr(), count, mpi.MPI_INT, op) == 0, count
+            assert torch.equal(inb, ref), ("inbuf modified", count)
+            assert torch.equal(io, want), ("inoutbuf", count, op)
+    assert lib.MPI_Op_free(ctypes.byref(uop)) == 0
+
+
 @pytest.mark.parametrize("op", ["MPI_SUM", "MPI_MAX", "MPI_MIN", "MPI_PROD"])
 @pytest.mark.parametrize("t", ["MPI_INT", "MPI_INT64_T", "MPI_FLOAT", "MPI_DOUBLE"])
 def test_config3_sweep_256mib(mpi, orc, cuda, op, t):

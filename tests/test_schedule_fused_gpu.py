@@ -165,3 +165,50 @@ def test_one_pass_combine_matches_stepwise_fold(mpi, orc, cuda, t, op, n, order)
     assert rc == 0, mpi.error_string(rc)
     torch.cuda.synchronize()
     assert same(out.cpu().numpy(), want, t)
+
+
+EVERY = [(op, t) for op in T.OPS for t in T.ALL_TYPES if T.compute_ok(op, t)]
+
+
+@pytest.mark.parametrize("op,t", EVERY, ids=[f"{o}-{t}" for o, t in EVERY])
+def test_every_pair_fused_matches_stepwise_fold(mpi, orc, cuda, op, t):
+    """Every (op, type) the reference computes, through MPIX_Reduce_local_multi:
+    TREE of 8 (one fused pass), CHAIN of 8 (one pass) and CHAIN of 5 (greedy
+    4 + 2 passes, the second reading the first's output) against the same
+    fold done one oracle MPIR_Reduce_local step at a time.  Operands with
+    specials (NaN, +-0, inf, denormals, extremes); the second round starts
+    every buffer one element past 256 B alignment so the fused kernel's head
+    and tail elements run too."""
+    torch = cuda
+    esz = T.elem_size(t)
+    dt, o = mpi.DATATYPES[t], mpi.OPS[op]
+    for k, (n, order) in enumerate(((8, "TREE"), (8, "CHAIN"), (5, "CHAIN"))):
+        for off in (0, esz):
+            count = 3000 + 7 * n + k
+            rng = np.random.default_rng(1000 * n + k + off)
+            xs = [T.to_bytes(T.gen(t, count, rng, op)) for _ in range(n)]
+            acc = [x.copy() for x in xs]
+            if order == "TREE":
+                step = 1
+                while step < n:
+                    for j in range(0, n, 2 * step):
+                        assert orc.reduce_local(acc[j + step], acc[j], count, dt, o, check=False) == 0
+                    step *= 2
+            else:
+                for j in range(1, n):
+                    assert orc.reduce_local(acc[j], acc[0], count, dt, o, check=False) == 0
+            nb = count * esz
+            dev = []
+            for x in xs:
+                d = torch.zeros(nb + off + 64, dtype=torch.uint8, device="cuda")
+                d[off:off + nb].copy_(torch.from_numpy(x))
+                dev.append(d)
+            out = torch.zeros(nb + off + 64, dtype=torch.uint8, device="cuda")
+            torch.cuda.synchronize()
+            rc = mpi.reduce_local_multi([d.data_ptr() + off for d in dev], out.data_ptr() + off, count, dt, o,
+                                        mpi.MPIX_ORDER_TREE if order == "TREE" else mpi.MPIX_ORDER_CHAIN)
+            assert rc == 0, mpi.error_string(rc)
+            torch.cuda.synchronize()
+            got = out[off:off + nb].cpu().numpy()
+            assert same(got, acc[0], t), f"n={n} {order} off={off}: {np.count_nonzero(got != acc[0])} bytes differ"
+            assert not out[:off].any() and not out[off + nb:].any(), "wrote outside the output"
