@@ -433,9 +433,9 @@ __device__ __forceinline__ T fold_fast(const T (&v0)[P]) {
     return v[0];
 }
 
-template <class Op, class T, int P, bool TREE, int U>
-__global__ __launch_bounds__(kThreads) void k_combine_multi(MultiArgs a) {
-    constexpr uint32_t tile = kThreads * U * 16;
+template <class Op, class T, int P, bool TREE, int U, int TH>
+__global__ __launch_bounds__(TH) void k_combine_multi(MultiArgs a) {
+    constexpr uint32_t tile = TH * U * 16;
     const uint64_t base = (uint64_t)blockIdx.x * tile;
     if (base < a.vbytes) {
         const uint64_t left = a.vbytes - base;
@@ -446,7 +446,7 @@ __global__ __launch_bounds__(kThreads) void k_combine_multi(MultiArgs a) {
             __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void *)(a.in[j] + base), 0, nrec, 0x00020000);
 #pragma unroll
             for (int u = 0; u < U; ++u)
-                x[j][u] = __builtin_amdgcn_raw_buffer_load_b128(r, (u * kThreads + (int)threadIdx.x) * 16, 0, kCachePolicyNT);
+                x[j][u] = __builtin_amdgcn_raw_buffer_load_b128(r, (u * TH + (int)threadIdx.x) * 16, 0, kCachePolicyNT);
         }
         __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc((void *)(a.out + base), 0, nrec, 0x00020000);
 #pragma unroll
@@ -463,7 +463,7 @@ __global__ __launch_bounds__(kThreads) void k_combine_multi(MultiArgs a) {
                 res.e[k] = fold_fast<Op, T, P, TREE>(v);
             }
             __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, res), ro,
-                                                   (u * kThreads + (int)threadIdx.x) * 16, 0, kCachePolicyNT);
+                                                   (u * TH + (int)threadIdx.x) * 16, 0, kCachePolicyNT);
         }
     }
     if (blockIdx.x == 0) {
@@ -495,9 +495,9 @@ __global__ __launch_bounds__(kThreads) void k_combine_multi_elems(MultiArgs a, u
     }
 }
 
-template <class Op, class T, int P, bool TREE, int U>
+template <class Op, class T, int P, bool TREE, int U, int TH>
 hipError_t launch_combine_pu(const void *const *ins, void *out_, uint64_t count, hipStream_t s) {
-    constexpr uint32_t tile = kThreads * U * 16;
+    constexpr uint32_t tile = TH * U * 16;
     char *out = static_cast<char *>(out_);
     const uintptr_t ao = reinterpret_cast<uintptr_t>(out);
     const uint64_t nbytes = count * sizeof(T);
@@ -521,7 +521,7 @@ hipError_t launch_combine_pu(const void *const *ins, void *out_, uint64_t count,
         a.tail_off = (int64_t)vbytes;
         uint64_t grid = (vbytes + tile - 1) / tile;
         if (grid == 0) grid = 1;
-        hipLaunchKernelGGL((k_combine_multi<Op, T, P, TREE, U>), dim3((unsigned)grid), dim3(kThreads), 0, s, a);
+        hipLaunchKernelGGL((k_combine_multi<Op, T, P, TREE, U, TH>), dim3((unsigned)grid), dim3(TH), 0, s, a);
     } else {
         a.out = out;
         a.vbytes = 0;
@@ -603,7 +603,7 @@ hipError_t launch_combine_any(const void *const *ins, int n, int tree, void *out
 
 template <class Op, class T, int P, bool TREE>
 hipError_t launch_combine_p(const void *const *ins, void *out_, uint64_t count, hipStream_t s) {
-    return launch_combine_pu<Op, T, P, TREE, (P >= 8 ? 1 : (P >= 4 ? 2 : 4))>(ins, out_, count, s);
+    return launch_combine_pu<Op, T, P, TREE, (P >= 8 ? 1 : (P >= 4 ? 2 : 4)), (P >= 8 ? 1024 : kThreads)>(ins, out_, count, s);
 }
 
 }  // namespace mpir_hip
