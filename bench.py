@@ -79,7 +79,7 @@ def time_steps(step, k: int, w: int, sync, barrier, max_over_ranks) -> float:
     return max_over_ranks(t1 - t0)
 
 
-def run_collectives_child(rank: int, world: int, local: int, barrier, timeout: float = 300.0):
+def run_collectives_child(rank: int, world: int, local: int, barrier, timeout: float = 180.0):
     """Configs 4-5 (Allreduce fp32 256 MiB, Reduce_scatter_block fp16 1 GiB) in a
     child process per rank with its own RCCL communicator, so a failure there
     cannot take this process's measurement down: the child is killed after
