@@ -211,7 +211,7 @@ int MPIX_Reduce_local_stream(const void *inbuf, void *inoutbuf, int count, MPI_D
 /* Multi-operand local reduction: outbuf = fold of n device buffers in ONE pass
  * over HBM, in the association a reduction schedule would produce by calling
  * MPIR_Reduce_local step by step (bit-identical to doing exactly that):
- *   MPIX_ORDER_TREE  (n = 1, 2, 4, 8): ((b0+b1)+(b2+b3))+((b4+b5)+(b6+b7)) --
+ *   MPIX_ORDER_TREE  (n a power of two <= 64): ((b0+b1)+(b2+b3))+((b4+b5)+(b6+b7)) --
  *       recursive halving, reduce_intra_reduce_scatter_gather.c:186-249;
  *   MPIX_ORDER_CHAIN (1 <= n <= 64): ((b0+b1)+b2)+... -- pairwise,
  *       reduce_scatter_block_intra_pairwise.c:97-134.
