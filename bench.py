@@ -16,7 +16,7 @@ torch.cuda.synchronize() on both sides, after W untimed warm-up steps.
             read inbuf, read inoutbuf, write inoutbuf -- SURVEY.md §8d)
 
 Extra fields (rank 0):
-  roofline      dominant kernel (k_reduce_tile<OpSum,float>): algorithmic bytes per
+  roofline      dominant kernel (k_reduce_tile_lean<OpSum,float>): algorithmic bytes per
                 launch / mean launch duration from HIP events recorded on the
                 stream the kernel runs on (MPIX_Reduce_local_stream onto a torch
                 stream), vs the 8.0 TB/s HBM3E peak; traffic = per-launch HBM
@@ -297,7 +297,7 @@ def main():
         traffic, tsrc = load_traffic(nbytes)
         out["roofline"] = {
             "bound": "hbm",
-            "kernel": "mpir_hip::k_reduce_tile<OpSum,float>",
+            "kernel": "mpir_hip::k_reduce_tile_lean<OpSum,float>",
             "achieved": round(achieved / 1e9, 1),
             "peak": HBM_PEAK_BPS / 1e9,
             "unit": "GB/s",

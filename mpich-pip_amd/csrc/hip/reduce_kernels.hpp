@@ -6,7 +6,8 @@
 // MI355X (256 MiB/operand fp32 SUM, profiles/ and DESIGN.md §Kernels):
 //
 //   * one 16 KiB tile per operand per 256-thread workgroup (4 x 16 B per lane,
-//     lane-contiguous 1 KiB wave-instructions), no grid-stride loop: the grid
+//     lane-contiguous 1 KiB wave-instructions, each wave a contiguous 4 KiB
+//     of the tile), no grid-stride loop: the grid
 //     is vbytes / 16 KiB workgroups (16384 at 256 MiB), which keeps every CU's
 //     queue deep and the DRAM pages of a tile together;
 //   * all 8 loads of a lane issued before the first combine (latency hiding
@@ -80,27 +81,46 @@ __device__ __forceinline__ u32x4 combine16(u32x4 a, u32x4 b) {
     }
 }
 
+// A short issue gap (s_nop 0, pinned in place by scheduling barriers) after
+// every (inout, in) pair of 16 B loads.  rocprofv3 kernel trace, 256 MiB fp32
+// SUM, same tile otherwise: 119.7 us (0.841 of the HBM peak) vs 124.2 us
+// (0.810) with the eight loads back to back (tools/shape_ab.hip,
+// profiles/r01s3_shape_ab.log); a gap after every load, or s_nop 3, measured
+// the same, s_nop 7 less.
+__device__ __forceinline__ void issue_gap() {
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_nop 0");
+    __builtin_amdgcn_sched_barrier(0);
+}
+
+// One 16 KiB tile per operand: each wave owns a contiguous 4 KiB of it (one
+// 1 KiB lane-contiguous access per instruction).
+template <class Op, class T>
+__device__ __forceinline__ void reduce_tile(const char *in, char *io, uint64_t base, uint64_t vbytes) {
+    const uint64_t left = vbytes - base;
+    const int nrec = (int)(left < kTileBytes ? left : kTileBytes);
+    __amdgpu_buffer_rsrc_t rin = __builtin_amdgcn_make_buffer_rsrc((void *)(in + base), 0, nrec, 0x00020000);
+    __amdgpu_buffer_rsrc_t rio = __builtin_amdgcn_make_buffer_rsrc((void *)(io + base), 0, nrec, 0x00020000);
+    const int t = (int)threadIdx.x;
+    const int wb = (t >> 6) * (kVecPerLane * 1024) + (t & 63) * 16;
+    u32x4 a[kVecPerLane], b[kVecPerLane];
+#pragma unroll
+    for (int u = 0; u < kVecPerLane; ++u) {
+        a[u] = __builtin_amdgcn_raw_buffer_load_b128(rio, wb + u * 1024, 0, kCachePolicyNT);
+        b[u] = __builtin_amdgcn_raw_buffer_load_b128(rin, wb + u * 1024, 0, kCachePolicyNT);
+        if (u + 1 < kVecPerLane) issue_gap();
+    }
+#pragma unroll
+    for (int u = 0; u < kVecPerLane; ++u)
+        __builtin_amdgcn_raw_buffer_store_b128(combine16<Op, T>(a[u], b[u]), rio, wb + u * 1024, 0, kCachePolicyNT);
+}
+
+// With head / tail elements (nhead or ntail != 0), workgroup 0 combines them
+// after its tile.
 template <class Op, class T>
 __device__ __forceinline__ void reduce_tile_body(const TileArgs<T> &args) {
     const uint64_t base = (uint64_t)blockIdx.x * kTileBytes;
-    if (base < args.vbytes) {
-        const uint64_t left = args.vbytes - base;
-        const int nrec = (int)(left < kTileBytes ? left : kTileBytes);
-        __amdgpu_buffer_rsrc_t rin = __builtin_amdgcn_make_buffer_rsrc((void *)(args.in + base), 0, nrec, 0x00020000);
-        __amdgpu_buffer_rsrc_t rio = __builtin_amdgcn_make_buffer_rsrc((void *)(args.io + base), 0, nrec, 0x00020000);
-        u32x4 a[kVecPerLane], b[kVecPerLane];
-#pragma unroll
-        for (int u = 0; u < kVecPerLane; ++u) {
-            const int off = (u * kThreads + (int)threadIdx.x) * 16;
-            a[u] = __builtin_amdgcn_raw_buffer_load_b128(rio, off, 0, kCachePolicyNT);
-            b[u] = __builtin_amdgcn_raw_buffer_load_b128(rin, off, 0, kCachePolicyNT);
-        }
-#pragma unroll
-        for (int u = 0; u < kVecPerLane; ++u) {
-            const int off = (u * kThreads + (int)threadIdx.x) * 16;
-            __builtin_amdgcn_raw_buffer_store_b128(combine16<Op, T>(a[u], b[u]), rio, off, 0, kCachePolicyNT);
-        }
-    }
+    if (base < args.vbytes) reduce_tile<Op, T>(args.in, args.io, base, args.vbytes);
     if (blockIdx.x == 0) {
         Op op;
         const unsigned t = threadIdx.x;
@@ -112,6 +132,15 @@ __device__ __forceinline__ void reduce_tile_body(const TileArgs<T> &args) {
 template <class Op, class T>
 __global__ __launch_bounds__(kThreads) void k_reduce_tile(TileArgs<T> args) {
     reduce_tile_body<Op, T>(args);
+}
+
+// No head / tail (the common case: 16 B-aligned buffers, bytes a multiple of
+// 16): three scalar arguments and nothing after the tile.
+template <class Op, class T>
+__global__ __launch_bounds__(kThreads) void k_reduce_tile_lean(const char *in, char *io, uint64_t vbytes) {
+    const uint64_t base = (uint64_t)blockIdx.x * kTileBytes;
+    if (base >= vbytes) return;
+    reduce_tile<Op, T>(in, io, base, vbytes);
 }
 
 // inbuf misaligned relative to inoutbuf: (in - io) mod 16 = delta != 0, the
@@ -179,6 +208,7 @@ __global__ __launch_bounds__(kThreads) void k_reduce_shift(ShiftArgs<T> args) {
             // at an offset past the descriptor's range (returns 0, no memory
             // request) -- a branch here would make the compiler drain vmcnt
             n63[u] = __builtin_amdgcn_raw_buffer_load_b128(rin, last_lane ? off + 16 : 0x40000000, 0, kCachePolicyNT);
+            if (u + 1 < kVecPerLane) issue_gap();
         }
 #pragma unroll
         for (int u = 0; u < kVecPerLane; ++u) {
@@ -259,7 +289,11 @@ hipError_t launch_reduce(const void *in_, void *io_, uint64_t count, hipStream_t
         a.ntail = (uint32_t)((rest - vbytes) / sizeof(T));
         uint64_t grid = (vbytes + kTileBytes - 1) / kTileBytes;
         if (grid == 0) grid = 1;
-        hipLaunchKernelGGL((k_reduce_tile<Op, T>), dim3((unsigned)grid), dim3(kThreads), 0, s, a);
+        if (a.nhead || a.ntail)
+            hipLaunchKernelGGL((k_reduce_tile<Op, T>), dim3((unsigned)grid), dim3(kThreads), 0, s, a);
+        else
+            hipLaunchKernelGGL((k_reduce_tile_lean<Op, T>), dim3((unsigned)grid), dim3(kThreads), 0, s, a.in, a.io,
+                               a.vbytes);
     } else if ((ao % alignof(T) == 0) && head0 % sizeof(T) == 0 && nbytes >= 2 * kTileBytes) {
         // inoutbuf element-aligned, inbuf at any other offset mod 16: the
         // aligned-load + shuffle + funnel tile kernel (small counts stay
@@ -321,6 +355,7 @@ __global__ __launch_bounds__(kThreads) void k_reduce_tile_wide(const char *in, c
     for (int v = 0; v < NV; ++v) {
         a[v] = __builtin_amdgcn_raw_buffer_load_b128(rio, (v * kThreads + t) * 16, 0, kCachePolicyNT);
         b[v] = __builtin_amdgcn_raw_buffer_load_b128(rin, (v * kThreads + t) * 16, 0, kCachePolicyNT);
+        if (v + 1 < NV) issue_gap();
     }
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
@@ -445,8 +480,10 @@ __global__ __launch_bounds__(TH) void k_combine_multi(MultiArgs a) {
         for (int j = 0; j < P; ++j) {
             __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void *)(a.in[j] + base), 0, nrec, 0x00020000);
 #pragma unroll
-            for (int u = 0; u < U; ++u)
+            for (int u = 0; u < U; ++u) {
                 x[j][u] = __builtin_amdgcn_raw_buffer_load_b128(r, (u * TH + (int)threadIdx.x) * 16, 0, kCachePolicyNT);
+                if (((j * U + u) & 1) && j * U + u + 1 < P * U) issue_gap();
+            }
         }
         __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc((void *)(a.out + base), 0, nrec, 0x00020000);
 #pragma unroll

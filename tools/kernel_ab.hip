@@ -151,11 +151,11 @@ int main(int argc, char **argv) {
     struct MVar { std::string name; size_t esz; hipError_t (*fn)(const void *const *, void *, uint64_t, hipStream_t); std::vector<float> ms; };
     std::vector<MVar> mvs = {
         {"TREE8 SUM fp32 U1 (product)", 4, &launch_combine_p<OpSum, float, 8, true>, {}},
-        {"TREE8 SUM fp32 U2", 4, &launch_combine_pu<OpSum, float, 8, true, 2>, {}},
-        {"TREE8 SUM fp32 U4", 4, &launch_combine_pu<OpSum, float, 8, true, 4>, {}},
-        {"TREE8 SUM fp32 U1 plain", 4, &launch_combine_pu<OpSumPlainM, float, 8, true, 1>, {}},
+        {"TREE8 SUM fp32 U2", 4, &launch_combine_pu<OpSum, float, 8, true, 2, 256>, {}},
+        {"TREE8 SUM fp32 U4", 4, &launch_combine_pu<OpSum, float, 8, true, 4, 256>, {}},
+        {"TREE8 SUM fp32 U1 plain", 4, &launch_combine_pu<OpSumPlainM, float, 8, true, 1, 256>, {}},
         {"CHAIN8 SUM fp16 U1 (product)", 2, &launch_combine_p<OpSum, f16, 8, false>, {}},
-        {"CHAIN8 SUM fp16 U2", 2, &launch_combine_pu<OpSum, f16, 8, false, 2>, {}},
+        {"CHAIN8 SUM fp16 U2", 2, &launch_combine_pu<OpSum, f16, 8, false, 2, 256>, {}},
         {"CHAIN8 SUM fp32 U1", 4, &launch_combine_p<OpSum, float, 8, false>, {}},
         {"TREE4 SUM fp32 U2 (product)", 4, &launch_combine_p<OpSum, float, 4, true>, {}},
         {"TREE2 SUM fp32 U4 (product)", 4, &launch_combine_p<OpSum, float, 2, true>, {}},

@@ -20,7 +20,7 @@ import os
 import statistics
 import sys
 
-KERNEL = "k_reduce_tile<mpir_hip::OpSum, float>"
+KERNEL = "k_reduce_tile_lean<mpir_hip::OpSum, float>"
 PEAK = 8.0e12
 
 
@@ -69,7 +69,7 @@ def main():
     hbm = int(round((2 * fetch_kb + write_kb) * 1024))
     achieved = alg / (avg_ns * 1e-9)
     d = {
-        "kernel": "mpir_hip::k_reduce_tile<OpSum,float>",
+        "kernel": "mpir_hip::k_reduce_tile_lean<OpSum,float>",
         "operand_bytes": operand_bytes,
         "algorithmic_bytes_per_launch": alg,
         "hbm_bytes_per_launch": hbm,
