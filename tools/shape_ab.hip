@@ -266,6 +266,45 @@ hipError_t launch_off(const void *in, void *io, uint64_t count, hipStream_t s) {
     return hipGetLastError();
 }
 
+// vectors per lane / workgroup size with the issue gap (NOP: s_nop count, -1 = no gap)
+template <int U, int TH, int NOP>
+__global__ __launch_bounds__(TH) void k_uv(const char *in, char *io, uint64_t vbytes) {
+    constexpr uint32_t tile = TH * U * 16;
+    const uint64_t base = (uint64_t)blockIdx.x * tile;
+    if (base >= vbytes) return;
+    const uint64_t left = vbytes - base;
+    const int nrec = (int)(left < tile ? left : tile);
+    __amdgpu_buffer_rsrc_t rin = __builtin_amdgcn_make_buffer_rsrc((void *)(in + base), 0, nrec, 0x00020000);
+    __amdgpu_buffer_rsrc_t rio = __builtin_amdgcn_make_buffer_rsrc((void *)(io + base), 0, nrec, 0x00020000);
+    const int t = (int)threadIdx.x;
+    const int wb = (t >> 6) * (U * 1024) + (t & 63) * 16;
+    u32x4 x[U], y[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        x[u] = __builtin_amdgcn_raw_buffer_load_b128(rio, wb + u * 1024, 0, kCachePolicyNT);
+        y[u] = __builtin_amdgcn_raw_buffer_load_b128(rin, wb + u * 1024, 0, kCachePolicyNT);
+        if constexpr (NOP >= 0) {
+            if (u + 1 < U) {
+                __builtin_amdgcn_sched_barrier(0);
+                if constexpr (NOP == 0) asm volatile("s_nop 0");
+                if constexpr (NOP == 1) asm volatile("s_nop 1");
+                if constexpr (NOP == 3) asm volatile("s_nop 3");
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+        __builtin_amdgcn_raw_buffer_store_b128(combine16<OpSum, float>(x[u], y[u]), rio, wb + u * 1024, 0, kCachePolicyNT);
+}
+template <int U, int TH, int NOP>
+hipError_t launch_uv(const void *in, void *io, uint64_t count, hipStream_t s) {
+    constexpr uint32_t tile = TH * U * 16;
+    hipLaunchKernelGGL((k_uv<U, TH, NOP>), dim3((unsigned)((count * 4 + tile - 1) / tile)), dim3(TH), 0, s,
+                       (const char *)in, (char *)io, count * 4);
+    return hipGetLastError();
+}
+
 struct Var { std::string name; hipError_t (*fn)(const void *, void *, uint64_t, hipStream_t); std::vector<float> ms; };
 
 int main(int argc, char **argv) {
@@ -285,15 +324,14 @@ int main(int argc, char **argv) {
     }
     std::vector<Var> vs = {
         {"product", &launch_reduce<OpSum, float>, {}},
-        {"wave", &launch_var<256, V_WAVE>, {}},
-        {"off IMM", &launch_off<false>, {}},
-        {"off IMM gap1", &launch_off<false, 1>, {}},
-        {"off IMM gap2", &launch_off<false, 2>, {}},
-        {"gap3 each load", &launch_off<false, 3>, {}},
-        {"gap4 pair nop3", &launch_off<false, 4>, {}},
-        {"gap5 pair nop7", &launch_off<false, 5>, {}},
-        {"gap6 pair+stores", &launch_off<false, 6>, {}},
-        {"product (again)", &launch_reduce<OpSum, float>, {}},
+        {"U4 T256 nogap", &launch_uv<4, 256, -1>, {}},
+        {"U4 T256 nop1", &launch_uv<4, 256, 1>, {}},
+        {"U2 T256 nop0", &launch_uv<2, 256, 0>, {}},
+        {"U8 T256 nop0", &launch_uv<8, 256, 0>, {}},
+        {"U8 T256 nop3", &launch_uv<8, 256, 3>, {}},
+        {"U4 T512 nop0", &launch_uv<4, 512, 0>, {}},
+        {"U2 T512 nop0", &launch_uv<2, 512, 0>, {}},
+        {"U4 T128 nop0", &launch_uv<4, 128, 0>, {}},
     };
     hipStream_t st;
     CK(hipStreamCreate(&st));
