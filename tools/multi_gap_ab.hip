@@ -1,0 +1,124 @@
+// multi_gap_ab.hip -- A/B of the fused 8-operand combine (config 4's TREE8 fp32
+// SUM and config 5's CHAIN8 fp16 SUM, 32 MiB blocks) over workgroup size,
+// vectors per lane and the load issue gap.  Run under
+//   rocprofv3 --kernel-trace -- tools/multi_gap_ab [MiB=32] [rounds=30]
+// and read the kernel durations from the trace (event brackets include the
+// host submit gap).  Variant order is shuffled every round; two operand sets
+// alternate (> Infinity Cache).
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off \
+//         -Impich-pip_amd/csrc/hip -o tools/multi_gap_ab tools/multi_gap_ab.hip
+#include <hip/hip_runtime.h>
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <string>
+#include <vector>
+
+#include "reduce_kernels.hpp"
+
+#define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { \
+    fprintf(stderr, "HIP %s at %s:%d\n", hipGetErrorString(e_), __FILE__, __LINE__); exit(2);} } while (0)
+
+using namespace mpir_hip;
+
+// GAP: a gap after every GAP loads (0 = none)
+template <class T, bool TREE, int P, int U, int TH, int GAP>
+__global__ __launch_bounds__(TH) void k_mx(MultiArgs a) {
+    constexpr uint32_t tile = TH * U * 16;
+    const uint64_t base = (uint64_t)blockIdx.x * tile;
+    if (base >= a.vbytes) return;
+    const uint64_t left = a.vbytes - base;
+    const int nrec = (int)(left < tile ? left : tile);
+    const int t = (int)threadIdx.x;
+    const int wb = (t >> 6) * (U * 1024) + (t & 63) * 16;
+    u32x4 x[P][U];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int j = 0; j < P; ++j) {
+            __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void *)(a.in[j] + base), 0, nrec, 0x00020000);
+            x[j][u] = __builtin_amdgcn_raw_buffer_load_b128(r, wb + u * 1024, 0, kCachePolicyNT);
+            if constexpr (GAP > 0) {
+                if ((u * P + j + 1) % GAP == 0 && u * P + j + 1 < U * P) issue_gap();
+            }
+        }
+    __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc((void *)(a.out + base), 0, nrec, 0x00020000);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        Pack16<T> pk[P];
+#pragma unroll
+        for (int j = 0; j < P; ++j) pk[j] = __builtin_bit_cast(Pack16<T>, x[j][u]);
+        Pack16<T> res;
+#pragma unroll
+        for (int k = 0; k < (int)(16 / sizeof(T)); ++k) {
+            T v[P];
+#pragma unroll
+            for (int j = 0; j < P; ++j) v[j] = pk[j].e[k];
+            res.e[k] = fold_fast<OpSum, T, P, TREE>(v);
+        }
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, res), ro, wb + u * 1024, 0, kCachePolicyNT);
+    }
+}
+
+typedef hipError_t (*mfn)(const void *const *, void *, uint64_t, hipStream_t);
+
+template <class T, bool TREE, int U, int TH, int GAP>
+hipError_t launch_mx(const void *const *ins, void *out, uint64_t count, hipStream_t s) {
+    MultiArgs a{};
+    for (int j = 0; j < 8; ++j) a.in[j] = static_cast<const char *>(ins[j]);
+    a.out = static_cast<char *>(out);
+    a.vbytes = count * sizeof(T);
+    constexpr uint32_t tile = TH * U * 16;
+    hipLaunchKernelGGL((k_mx<T, TREE, 8, U, TH, GAP>), dim3((unsigned)((a.vbytes + tile - 1) / tile)), dim3(TH), 0, s, a);
+    return hipGetLastError();
+}
+
+struct Var { std::string name; size_t esz; mfn fn; };
+
+int main(int argc, char **argv) {
+    size_t mib = argc > 1 ? strtoull(argv[1], 0, 10) : 32;
+    int rounds = argc > 2 ? atoi(argv[2]) : 30;
+    size_t bytes = mib << 20;
+    const int P = 8, NS = 2;
+    std::vector<char *> ins(P * NS), outs(NS);
+    std::vector<uint32_t> h(bytes / 4);
+    uint32_t x = 0x5EED;
+    for (auto &v : h) { x ^= x << 13; x ^= x >> 17; x ^= x << 5; v = 0x3c003c00u | (x & 0x03ff03ffu); }  // finite fp16 / fp32
+    for (auto &p : ins) { CK(hipMalloc(&p, bytes)); CK(hipMemcpy(p, h.data(), bytes, hipMemcpyHostToDevice)); }
+    for (auto &p : outs) CK(hipMalloc(&p, bytes));
+    std::vector<Var> vs = {
+        {"TREE8 f32 product", 4, &launch_combine_p<OpSum, float, 8, true>},
+        {"TREE8 f32 U1 T1024 nogap", 4, &launch_mx<float, true, 1, 1024, 0>},
+        {"TREE8 f32 U1 T1024 gap2", 4, &launch_mx<float, true, 1, 1024, 2>},
+        {"TREE8 f32 U1 T1024 gap1", 4, &launch_mx<float, true, 1, 1024, 1>},
+        {"TREE8 f32 U1 T256 gap2", 4, &launch_mx<float, true, 1, 256, 2>},
+        {"TREE8 f32 U2 T256 gap2", 4, &launch_mx<float, true, 2, 256, 2>},
+        {"TREE8 f32 U2 T512 gap2", 4, &launch_mx<float, true, 2, 512, 2>},
+        {"TREE8 f32 U1 T512 gap2", 4, &launch_mx<float, true, 1, 512, 2>},
+        {"TREE8 f32 U1 T1024 gap4", 4, &launch_mx<float, true, 1, 1024, 4>},
+        {"CHAIN8 f16 product", 2, &launch_combine_p<OpSum, f16, 8, false>},
+        {"CHAIN8 f16 U1 T1024 gap1", 2, &launch_mx<f16, false, 1, 1024, 1>},
+        {"CHAIN8 f16 U2 T512 gap2", 2, &launch_mx<f16, false, 2, 512, 2>},
+    };
+    hipStream_t st;
+    CK(hipStreamCreate(&st));
+    std::vector<int> order(vs.size());
+    for (size_t i = 0; i < order.size(); ++i) order[i] = (int)i;
+    uint32_t rs = 777;
+    int slot = 0;
+    for (int r = -2; r < rounds; ++r) {
+        for (size_t i = order.size() - 1; i > 0; --i) {
+            rs = rs * 1664525u + 1013904223u;
+            std::swap(order[i], order[(rs >> 8) % (i + 1)]);
+        }
+        for (int vi : order) {
+            const int s = slot++ % NS;
+            const void *ptr[P];
+            for (int j = 0; j < P; ++j) ptr[j] = ins[s * P + j];
+            CK(vs[vi].fn(ptr, outs[s], bytes / vs[vi].esz, st));
+            CK(hipStreamSynchronize(st));
+        }
+    }
+    printf("8 x %zu MiB -> 1, %d rounds; durations: see the rocprofv3 kernel trace\n", mib, rounds);
+    return 0;
+}
