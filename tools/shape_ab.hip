@@ -305,6 +305,50 @@ hipError_t launch_uv(const void *in, void *io, uint64_t count, hipStream_t s) {
     return hipGetLastError();
 }
 
+// refinements of the issue gap: MODE 0 product shape (io, in, nop 0);
+// 1 in-first pairs; 2 odd waves s_sleep 1 at start; 3 s_nop 1; 4 s_nop 2
+template <int MODE>
+__global__ __launch_bounds__(256) void k_g(const char *in, char *io, uint64_t vbytes) {
+    const uint64_t base = (uint64_t)blockIdx.x * kTileBytes;
+    if (base >= vbytes) return;
+    const uint64_t left = vbytes - base;
+    const int nrec = (int)(left < kTileBytes ? left : kTileBytes);
+    __amdgpu_buffer_rsrc_t rin = __builtin_amdgcn_make_buffer_rsrc((void *)(in + base), 0, nrec, 0x00020000);
+    __amdgpu_buffer_rsrc_t rio = __builtin_amdgcn_make_buffer_rsrc((void *)(io + base), 0, nrec, 0x00020000);
+    const int t = (int)threadIdx.x;
+    if constexpr (MODE == 2) {
+        if ((t >> 6) & 1) __builtin_amdgcn_s_sleep(1);
+    }
+    const int wb = (t >> 6) * 4096 + (t & 63) * 16;
+    u32x4 x[4], y[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        if constexpr (MODE == 1) {
+            y[u] = __builtin_amdgcn_raw_buffer_load_b128(rin, wb + u * 1024, 0, kCachePolicyNT);
+            x[u] = __builtin_amdgcn_raw_buffer_load_b128(rio, wb + u * 1024, 0, kCachePolicyNT);
+        } else {
+            x[u] = __builtin_amdgcn_raw_buffer_load_b128(rio, wb + u * 1024, 0, kCachePolicyNT);
+            y[u] = __builtin_amdgcn_raw_buffer_load_b128(rin, wb + u * 1024, 0, kCachePolicyNT);
+        }
+        if (u < 3) {
+            __builtin_amdgcn_sched_barrier(0);
+            if constexpr (MODE == 3) asm volatile("s_nop 1");
+            else if constexpr (MODE == 4) asm volatile("s_nop 2");
+            else asm volatile("s_nop 0");
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+        __builtin_amdgcn_raw_buffer_store_b128(combine16<OpSum, float>(x[u], y[u]), rio, wb + u * 1024, 0, kCachePolicyNT);
+}
+template <int MODE>
+hipError_t launch_g(const void *in, void *io, uint64_t count, hipStream_t s) {
+    hipLaunchKernelGGL((k_g<MODE>), dim3((unsigned)((count * 4 + kTileBytes - 1) / kTileBytes)), dim3(256), 0, s,
+                       (const char *)in, (char *)io, count * 4);
+    return hipGetLastError();
+}
+
 struct Var { std::string name; hipError_t (*fn)(const void *, void *, uint64_t, hipStream_t); std::vector<float> ms; };
 
 int main(int argc, char **argv) {
@@ -324,14 +368,12 @@ int main(int argc, char **argv) {
     }
     std::vector<Var> vs = {
         {"product", &launch_reduce<OpSum, float>, {}},
+        {"g0 same as product", &launch_g<0>, {}},
+        {"g1 in-first", &launch_g<1>, {}},
+        {"g2 odd-wave sleep", &launch_g<2>, {}},
+        {"g3 nop1", &launch_g<3>, {}},
+        {"g4 nop2", &launch_g<4>, {}},
         {"U4 T256 nogap", &launch_uv<4, 256, -1>, {}},
-        {"U4 T256 nop1", &launch_uv<4, 256, 1>, {}},
-        {"U2 T256 nop0", &launch_uv<2, 256, 0>, {}},
-        {"U8 T256 nop0", &launch_uv<8, 256, 0>, {}},
-        {"U8 T256 nop3", &launch_uv<8, 256, 3>, {}},
-        {"U4 T512 nop0", &launch_uv<4, 512, 0>, {}},
-        {"U2 T512 nop0", &launch_uv<2, 512, 0>, {}},
-        {"U4 T128 nop0", &launch_uv<4, 128, 0>, {}},
     };
     hipStream_t st;
     CK(hipStreamCreate(&st));
