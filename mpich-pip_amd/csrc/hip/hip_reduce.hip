@@ -47,22 +47,21 @@ constexpr int kMaxStageSlots = 8;
 // stages of one chunk and stop a slot from being refilled before its
 // copy-back has read it.
 // MPIR_CVAR_REDUCE_LOCAL_STAGE_CHUNK_MB / MPIR_CVAR_REDUCE_LOCAL_STAGE_SLOTS override.
+// (function-local statics: initialised once, thread-safe)
 uint64_t stage_chunk() {
-    static uint64_t v = 0;
-    if (!v) {
+    static const uint64_t v = [] {
         const char *e = getenv("MPIR_CVAR_REDUCE_LOCAL_STAGE_CHUNK_MB");
         const long mb = e ? atol(e) : 0;
-        v = (uint64_t)(mb > 0 && mb <= 1024 ? mb : 32) << 20;
-    }
+        return (uint64_t)(mb > 0 && mb <= 1024 ? mb : 32) << 20;
+    }();
     return v;
 }
 int stage_slots() {
-    static int v = 0;
-    if (!v) {
+    static const int v = [] {
         const char *e = getenv("MPIR_CVAR_REDUCE_LOCAL_STAGE_SLOTS");
         const int n = e ? atoi(e) : 0;
-        v = n >= 2 && n <= kMaxStageSlots ? n : 3;
-    }
+        return n >= 2 && n <= kMaxStageSlots ? n : 3;
+    }();
     return v;
 }
 
@@ -195,11 +194,10 @@ Loc classify(const void *p, int *dev) {
 // The spin re-checks hipStreamQuery every 64Ki polls so a faulted stream
 // returns an error instead of spinning forever.
 int wait_mode() {
-    static int mode = -1;
-    if (mode < 0) {
+    static const int mode = [] {
         const char *v = getenv("MPIR_CVAR_REDUCE_LOCAL_WAIT");
-        mode = (v && !strcmp(v, "block")) ? 0 : 1;
-    }
+        return (v && !strcmp(v, "block")) ? 0 : 1;
+    }();
     return mode;
 }
 

@@ -164,13 +164,16 @@ int MPIR_Err_return(const char *fcname, int mpi_errno)
 
 static int alias_check_enabled(void)
 {
-    /* MPIR_CVAR_COLL_ALIAS_CHECK (mpir_err.h:157-171), default 1 */
+    /* MPIR_CVAR_COLL_ALIAS_CHECK (mpir_err.h:157-171), default 1.  Racing
+     * first calls store the same value; the atomics make that well defined. */
     static int cached = -1;
-    if (cached < 0) {
+    int c = __atomic_load_n(&cached, __ATOMIC_RELAXED);
+    if (c < 0) {
         const char *v = getenv("MPIR_CVAR_COLL_ALIAS_CHECK");
-        cached = v ? (atoi(v) != 0) : 1;
+        c = v ? (atoi(v) != 0) : 1;
+        __atomic_store_n(&cached, c, __ATOMIC_RELAXED);
     }
-    return cached;
+    return c;
 }
 
 /* The validation block of MPI_Reduce_local (reduce_local.c:166-191). */
