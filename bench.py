@@ -240,9 +240,14 @@ def main():
     ptrs = [(a.data_ptr(), b.data_ptr()) for a, b in pairs]
     sync()
 
+    # MPI_Reduce_local through the compiled binding (csrc/py/fastcall.c), the
+    # way mpi4py calls MPI: ~0.25 us of Python per call instead of ~1.2 us (ctypes)
+    reduce_local = m.fast_reduce_local()
+    dt_f32, op_sum = m.MPI_FLOAT, m.MPI_SUM
+
     def step(i):
         pin, pio = ptrs[i % NPAIRS]
-        rc = lib.MPI_Reduce_local(pin, pio, count, m.MPI_FLOAT, m.MPI_SUM)
+        rc = reduce_local(pin, pio, count, dt_f32, op_sum)
         if rc:
             raise RuntimeError(m.error_string(rc))
 
@@ -267,7 +272,7 @@ def main():
                         "device-resident, one rank per GPU" % (args.mib, count),
             "count": count,
             "algorithmic_bytes_per_call": alg_bytes,
-            "api": "MPI_Reduce_local (C ABI, synchronous)",
+            "api": "MPI_Reduce_local (C ABI, synchronous; called through the compiled CPython binding)",
             "parallelism": "replica-per-gpu (no data-path collective)",
         },
         # the synchronous call per GPU (launch + completion included) against the HBM peak

@@ -1,0 +1,50 @@
+/*
+ * fastcall.c -- CPython binding of MPI_Reduce_local for the Python side
+ * (bench.py, tests): one METH_FASTCALL function that unpacks five integers and
+ * calls the C ABI directly, ~0.1 us per call against ~1.2 us through ctypes.
+ * The way mpi4py binds MPI (compiled, not libffi); no compute of its own.
+ *
+ *   _fastcall.reduce_local(inbuf_addr, inoutbuf_addr, count, datatype, op) -> int
+ */
+#define PY_SSIZE_T_CLEAN
+#include <Python.h>
+#include <limits.h>
+
+#include "mpi_reduce_local.h"
+
+static PyObject *fc_reduce_local(PyObject *self, PyObject *const *args, Py_ssize_t nargs)
+{
+    (void) self;
+    if (nargs != 5) {
+        PyErr_SetString(PyExc_TypeError, "reduce_local(inbuf, inoutbuf, count, datatype, op)");
+        return NULL;
+    }
+    const void *in = PyLong_AsVoidPtr(args[0]);
+    void *io = PyLong_AsVoidPtr(args[1]);
+    const long count = PyLong_AsLong(args[2]);
+    const long dt = PyLong_AsLong(args[3]);
+    const long op = PyLong_AsLong(args[4]);
+    if (PyErr_Occurred())
+        return NULL;
+    if (count < INT_MIN || count > INT_MAX) {
+        PyErr_SetString(PyExc_OverflowError, "count does not fit the C int of MPI_Reduce_local");
+        return NULL;
+    }
+    return PyLong_FromLong(MPI_Reduce_local(in, io, (int) count, (MPI_Datatype) dt, (MPI_Op) op));
+}
+
+static PyMethodDef fc_methods[] = {
+    {"reduce_local", (PyCFunction) (void (*)(void)) fc_reduce_local, METH_FASTCALL,
+     "MPI_Reduce_local(inbuf, inoutbuf, count, datatype, op) on raw addresses; returns the MPI error code"},
+    {NULL, NULL, 0, NULL}
+};
+
+static struct PyModuleDef fc_module = {
+    PyModuleDef_HEAD_INIT, "_fastcall", "Compiled binding of MPI_Reduce_local", -1, fc_methods,
+    NULL, NULL, NULL, NULL
+};
+
+PyMODINIT_FUNC PyInit__fastcall(void)
+{
+    return PyModule_Create(&fc_module);
+}

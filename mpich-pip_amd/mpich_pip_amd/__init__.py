@@ -204,6 +204,17 @@ def error_string(code: int) -> str:
     return buf.value.decode(errors="replace")
 
 
+def fast_reduce_local():
+    """The compiled binding of MPI_Reduce_local (csrc/py/fastcall.c, METH_FASTCALL):
+    f(inbuf, inoutbuf, count, datatype, op) -> error code, ~0.25 us of Python
+    overhead per call against ~1.2 us through ctypes.  Same library instance as
+    load() (it is loaded first, so the errhandler and per-thread state are shared).
+    Raises if the extension was not built."""
+    load()
+    from . import _fastcall
+    return _fastcall.reduce_local
+
+
 def reduce_local(inbuf: int, inoutbuf: int, count: int, datatype: int, op: int) -> int:
     """MPI_Reduce_local on raw addresses (device or host)."""
     return load().MPI_Reduce_local(ctypes.c_void_p(inbuf), ctypes.c_void_p(inoutbuf), count, datatype, op)

@@ -217,3 +217,24 @@ def test_public_headers_compile_and_link(mpi, tmp_path, compiler):
                     os.path.join(root, "tests", "progs", "abi_link.c"), "-o", exe, "-L" + lib,
                     "-lmpich_reduce_local", "-Wl,-rpath," + lib], check=True)
     assert subprocess.run([exe]).returncode == 0
+
+
+def test_fastcall_binding_same_library_and_errors(mpi):
+    """The compiled CPython binding bench.py times MPI_Reduce_local through
+    (csrc/py/fastcall.c) calls the same library instance as ctypes: the
+    validation classes match call for call (no device work on these paths)."""
+    f = mpi.fast_reduce_local()
+    a = np.zeros(4, np.float32)
+    b = np.zeros(4, np.float32)
+    cases = [
+        (b.ctypes.data, a.ctypes.data, 4, mpi.MPI_FLOAT, mpi.MPI_BAND),      # op/type mismatch
+        (a.ctypes.data, a.ctypes.data, 4, mpi.MPI_FLOAT, mpi.MPI_SUM),       # alias
+        (b.ctypes.data, a.ctypes.data, 0, mpi.MPI_FLOAT, mpi.MPI_SUM),       # count 0
+        (b.ctypes.data, a.ctypes.data, 4, mpi.MPI_FLOAT, mpi.MPI_OP_NULL),   # null op
+    ]
+    for c in cases:
+        assert f(*c) == mpi.reduce_local(*c), c
+    with pytest.raises(OverflowError):
+        f(0, 0, 1 << 40, mpi.MPI_FLOAT, mpi.MPI_SUM)
+    with pytest.raises(TypeError):
+        f(0, 0, 1)
