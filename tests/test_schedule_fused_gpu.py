@@ -212,3 +212,40 @@ def test_every_pair_fused_matches_stepwise_fold(mpi, orc, cuda, op, t):
             got = out[off:off + nb].cpu().numpy()
             assert same(got, acc[0], t), f"n={n} {order} off={off}: {np.count_nonzero(got != acc[0])} bytes differ"
             assert not out[:off].any() and not out[off + nb:].any(), "wrote outside the output"
+
+
+@pytest.mark.parametrize("t,order,block_mib", [("MPI_FLOAT", "TREE", 32), ("MPIX_C_FLOAT16", "CHAIN", 128)],
+                         ids=["config4-tree8-fp32-32MiB", "config5-chain8-fp16-128MiB"])
+def test_fused_full_size_blocks(mpi, orc, cuda, t, order, block_mib):
+    """The fused combines at the block sizes of BASELINE configs 4-5 at N = 8
+    (Allreduce 256 MiB -> 8 x 32 MiB blocks, TREE; Reduce_scatter_block 1 GiB
+    fp16 -> 8 x 128 MiB blocks, CHAIN), bit-exact against the oracle's
+    step-by-step fold over the whole block."""
+    torch = cuda
+    esz = T.elem_size(t)
+    n = (block_mib << 20) // esz
+    dt, o = mpi.DATATYPES[t], mpi.OPS["MPI_SUM"]
+    g = torch.Generator(device="cuda").manual_seed(block_mib)
+    if t == "MPI_FLOAT":
+        dev = [torch.rand(n, device="cuda", generator=g) * 2 - 1 for _ in range(8)]
+    else:
+        dev = [(torch.rand(n, device="cuda", generator=g) * 8 - 4).half() for _ in range(8)]
+    out = torch.empty_like(dev[0])
+    torch.cuda.synchronize()
+    rc = mpi.reduce_local_multi([d.data_ptr() for d in dev], out.data_ptr(), n, dt, o,
+                                mpi.MPIX_ORDER_TREE if order == "TREE" else mpi.MPIX_ORDER_CHAIN)
+    assert rc == 0, mpi.error_string(rc)
+    torch.cuda.synchronize()
+    acc = [d.cpu().numpy().view(np.uint8).copy() for d in dev]
+    del dev
+    if order == "TREE":
+        step = 1
+        while step < 8:
+            for j in range(0, 8, 2 * step):
+                assert orc.reduce_local(acc[j + step], acc[j], n, dt, o, check=False) == 0
+            step *= 2
+    else:
+        for j in range(1, 8):
+            assert orc.reduce_local(acc[j], acc[0], n, dt, o, check=False) == 0
+    got = out.cpu().numpy().view(np.uint8)
+    assert np.array_equal(got, acc[0]), f"{np.count_nonzero(got != acc[0])} bytes differ"
