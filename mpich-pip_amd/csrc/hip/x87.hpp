@@ -166,6 +166,30 @@ X87_FN x80 x80_addsub(x80 a, x80 b, bool sub, const x80 &pad) {
         const bool sticky = (y & (((u128)1 << d) - 1)) != 0;
         y = (y >> d) | (sticky ? 1 : 0);
     }
+    // Fast path: the larger significand has its integer bit (x in [2^126,
+    // 2^127)), and either the signs agree or the exponents differ by >= 2, so
+    // the result's leading one is at bit 127, 126 or 125 and the rounding
+    // position is one of three fixed shifts (no 128-bit shifter, no clz).
+    // Same rounding as x80_round_pack: the sticky bit sits in bit 0, far below.
+    if ((ma >> 63) && (sa == sb || d >= 2)) {
+        const u128 s = sa == sb ? x + y : x - y;
+        const uint64_t hi = (uint64_t)(s >> 64), lo = (uint64_t)s;
+        int p;
+        uint64_t sig, rem, half;
+        if (hi >> 63) { p = 127; sig = hi; rem = lo; half = 1ull << 63; }
+        else if (hi >> 62) { p = 126; sig = (hi << 1) | (lo >> 63); rem = lo & ~(1ull << 63); half = 1ull << 62; }
+        else { p = 125; sig = (hi << 2) | (lo >> 62); rem = lo & ((1ull << 62) - 1); half = 1ull << 61; }
+        int er = ea - 126 + p + 16383;
+        if (er >= 1 && er <= 0x7ffe) {
+            if (rem > half || (rem == half && (sig & 1))) {
+                if (++sig == 0) {
+                    sig = 1ull << 63;
+                    if (++er >= 0x7fff) return x80_make(sa, 0x7fff, 1ull << 63, pad);
+                }
+            }
+            return x80_make(sa, (uint32_t)er, sig, pad);
+        }
+    }
     if (sa == sb) return x80_round_pack(sa, ea - 126, x + y, pad);
     const u128 s = x - y;
     if (s == 0) return x80_make(0, 0, 0, pad);      // exact cancellation: +0 (round to nearest)
