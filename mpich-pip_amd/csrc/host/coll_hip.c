@@ -344,6 +344,19 @@ static int group_exchange(struct MPIX_Hip_comm_s *c, const xfer_t *sends, int ns
 }
 
 /* ------------------------------------------------------------ helpers */
+/* Byte stride between staging slots.  Slots at a power-of-two stride (equal
+ * blocks of a power-of-two message) put the P operand streams of a fused
+ * combine on the same HBM channels at the same moment: 8 x 32 MiB TREE8 fp32
+ * ran at 0.689 of the HBM peak with a 32 MiB stride, 0.767 with 32 MiB +
+ * 4352 B (4 KiB + 256), 0.717 with + 256 B only (rocprofv3 kernel trace,
+ * tools/multi_gap_ab.hip, profiles/r01s3_multi_skew_ab.log).  The skew keeps
+ * the 256 B alignment (fused kernels need the operands equal mod 16). */
+static size_t stage_stride(size_t bytes)
+{
+    size_t st = (bytes + 255) & ~(size_t) 255;
+    return st >= ((size_t) 1 << 20) ? st + 4352 : st;
+}
+
 static int pof2_of(int p)
 {
     int q = 1;
@@ -449,7 +462,7 @@ static int allreduce_short(struct MPIX_Hip_comm_s *c, const void *sendbuf, void 
                            size_t esz, int opidx, int elem, hipStream_t s, const char *fc)
 {
     int p = c->size, q, nx = 0, rc = MPI_SUCCESS, mask;
-    size_t bytes = (size_t) count * esz, slot = (bytes + 255) & ~(size_t) 255;
+    size_t bytes = (size_t) count * esz, slot = stage_stride(bytes);
     xfer_t sends[MAX_XFER], recvs[MAX_XFER];
     const void *ys[64];
     char *scr = NULL, *own;
@@ -500,7 +513,7 @@ static int allreduce_recursive_doubling(struct MPIX_Hip_comm_s *c, const void *s
                                         const char *fc)
 {
     int p = c->size, q, nx = 0, rc = MPI_SUCCESS, pof2 = pof2_of(p), rem = p - pof2, n, j, m;
-    size_t bytes = (size_t) count * esz, slot = (bytes + 255) & ~(size_t) 255;
+    size_t bytes = (size_t) count * esz, slot = stage_stride(bytes);
     xfer_t sends[MAX_XFER], recvs[MAX_XFER];
     const void *ys[64];
     char *scr = NULL, *own;
@@ -549,7 +562,7 @@ static int reduce_scatter_short(struct MPIX_Hip_comm_s *c, const char *src, void
 {
     int p = c->size, q, nx = 0, rc = MPI_SUCCESS, pof2 = pof2_of(p), rem = p - pof2, bits = 0, n, k, m;
     long rcount = cnts[c->rank];
-    size_t nb = (size_t) rcount * esz, slot = (nb + 255) & ~(size_t) 255;
+    size_t nb = (size_t) rcount * esz, slot = stage_stride(nb);
     xfer_t sends[MAX_XFER], recvs[MAX_XFER];
     const void *ys[64];
     char *scr = NULL;
@@ -667,15 +680,21 @@ static int want_rccl(struct MPIX_Hip_comm_s *c, int algorithm, int elem, int opi
  * then the recursive halving (:186-249) as ONE all-to-all of blocks and ONE
  * fused tree combine: newrank n owns block bitrev(n), reduced as
  * ((y0+y1)+(y2+y3))+... with y_j = the block from newrank n ^ j.
- * `scr` holds (pof2-1) * cnts[0] elements + count elements + 256 bytes.
+ * `scr` holds rsg_scratch_bytes(): (pof2-1) slots of stage_stride(cnts[0]
+ * elements), then `count` elements for the pre-fold partner's vector.
  * Returns this rank's newrank in *newrank (-1: excluded by the pre-fold). */
+
+static size_t rsg_scratch_bytes(int pof2, const long *cnts, size_t esz, size_t bytes)
+{
+    return (size_t) (pof2 > 1 ? pof2 - 1 : 1) * stage_stride((size_t) cnts[0] * esz) + bytes + 256;
+}
 
 static int rsg_phase(struct MPIX_Hip_comm_s *c, char *work, long count, size_t esz, int opidx, int elem,
                      hipStream_t s, const char *fc, char *scr, const long *cnts, const long *disps, int odd_keeps,
                      int *newrank)
 {
     int p = c->size, pof2 = pof2_of(p), rem = p - pof2, bits = 0, nsend = 0, nrecv = 0, rc, i;
-    size_t bytes = (size_t) count * esz, maxblk = (size_t) cnts[0];
+    size_t bytes = (size_t) count * esz, blk = stage_stride((size_t) cnts[0] * esz);
     xfer_t sends[MAX_XFER], recvs[MAX_XFER];
     while ((1 << bits) < pof2)
         bits++;
@@ -692,7 +711,7 @@ static int rsg_phase(struct MPIX_Hip_comm_s *c, char *work, long count, size_t e
                 return rc;
             *newrank = -1;
         } else {
-            char *tmp = scr + (size_t) (pof2 > 1 ? pof2 - 1 : 1) * maxblk * esz;
+            char *tmp = scr + (size_t) (pof2 > 1 ? pof2 - 1 : 1) * blk;
             xfer_t x = { tmp, bytes, odd_keeps ? c->rank - 1 : c->rank + 1 };
             if ((rc = group_exchange(c, NULL, 0, &x, 1, s)) != MPI_SUCCESS)
                 return rc;
@@ -716,7 +735,7 @@ static int rsg_phase(struct MPIX_Hip_comm_s *c, char *work, long count, size_t e
             sends[nsend].buf = work + disps[b] * esz;
             sends[nsend].bytes = (size_t) cnts[b] * esz;
             sends[nsend++].peer = real;
-            recvs[nrecv].buf = scr + (size_t) ((n ^ m) - 1) * maxblk * esz;
+            recvs[nrecv].buf = scr + (size_t) ((n ^ m) - 1) * blk;
             recvs[nrecv].bytes = (size_t) cnts[mb] * esz;
             recvs[nrecv++].peer = real;
         }
@@ -724,7 +743,7 @@ static int rsg_phase(struct MPIX_Hip_comm_s *c, char *work, long count, size_t e
             return rc;
         ys[0] = work + disps[mb] * esz;
         for (i = 1; i < pof2; i++)
-            ys[i] = scr + (size_t) (i - 1) * maxblk * esz;
+            ys[i] = scr + (size_t) (i - 1) * blk;
         if (cnts[mb] && (rc = fold_tree(ys, pof2, work + disps[mb] * esz, cnts[mb], opidx, elem, s, fc)))
             return rc;
     } else if (pof2 > 1) {
@@ -802,7 +821,7 @@ int MPIX_Allreduce_hip(const void *sendbuf, void *recvbuf, int count, MPI_Dataty
     while ((1 << bits) < pof2)
         bits++;
     cnts_disps(count, pof2, cnts, disps);
-    if (comm_scratch(c, (size_t) (pof2 - 1) * (size_t) cnts[0] * esz + bytes + 256, &scr)) {
+    if (comm_scratch(c, rsg_scratch_bytes(pof2, cnts, esz, bytes), &scr)) {
         MPIR_Err_set_detail("%s: scratch allocation failed", fc);
         rc = MPI_ERR_NO_MEM;
         goto done;
@@ -907,7 +926,7 @@ int MPIX_Reduce_hip(const void *sendbuf, void *recvbuf, int count, MPI_Datatype 
     if (bytes <= REDUCE_SHORT_MSG_SIZE || count < pof2) {
         /* binomial: slot rel holds x_{(rel + root) % p}; the tree folds relranks */
         int mask;
-        slot = (bytes + 255) & ~(size_t) 255;
+        slot = stage_stride(bytes);
         if (!isroot) {
             xfer_t x = { (void *) own, bytes, root };
             TRY(group_exchange(c, &x, 1, NULL, 0, s));
@@ -945,7 +964,7 @@ int MPIX_Reduce_hip(const void *sendbuf, void *recvbuf, int count, MPI_Datatype 
     while ((1 << bits) < pof2)
         bits++;
     cnts_disps(count, pof2, cnts, disps);
-    slot = ((size_t) (pof2 - 1) * (size_t) cnts[0] * esz + bytes + 256 + 255) & ~(size_t) 255;
+    slot = (rsg_scratch_bytes(pof2, cnts, esz, bytes) + 255) & ~(size_t) 255;
     if (comm_scratch(c, slot + (isroot ? 0 : bytes), &scr)) {
         MPIR_Err_set_detail("%s: scratch allocation failed", fc);
         rc = MPI_ERR_NO_MEM;
@@ -1057,7 +1076,7 @@ static int reduce_scatter_common(const char *fc, const void *sendbuf, void *recv
     }
     /* long: pairwise.  y_i = block r from rank r - i into scratch slot i-1; in
      * place, the own block is staged too when it overlaps the output. */
-    slot = (nb + 255) & ~(size_t) 255;
+    slot = stage_stride(nb);
     if (comm_scratch(c, (size_t) p * slot + 256, &scr)) {
         MPIR_Err_set_detail("%s: scratch allocation failed", fc);
         rc = MPI_ERR_NO_MEM;
@@ -1164,7 +1183,7 @@ static int scan_common(const char *fc, const void *sendbuf, void *recvbuf, int c
     s = hip_stream ? (hipStream_t) hip_stream : c->stream;
     esz = MPIR_Hip_elem_size(elem);
     bytes = (size_t) count * esz;
-    slot = (bytes + 255) & ~(size_t) 255;
+    slot = stage_stride(bytes);
     p = c->size;
     r = c->rank;
     own = sendbuf == MPI_IN_PLACE ? recvbuf : sendbuf;

@@ -385,3 +385,62 @@ def test_collective_validation(mpi, cuda):
         assert mpi.allreduce(a.data_ptr(), b.data_ptr(), 0, mpi.MPI_FLOAT, mpi.MPI_SUM, comms[0]) == 0
     finally:
         mpi.comm_free(comms[0])
+
+
+@pytest.mark.parametrize("p", [3, 8])
+def test_large_blocks_skewed_staging(mpi, orc, cuda, p):
+    """Messages whose staging slots are >= 1 MiB, where the slots sit at a
+    skewed (non-power-of-two) stride (coll_hip.c stage_stride): Allreduce and
+    Reduce (root 0 and p-1) through the reduce-scatter phase, Reduce_scatter_block
+    pairwise, Scan and Exscan -- fp32 SUM, bit-exact vs the step-by-step schedules."""
+    from oracle import schedules as S
+    torch = cuda
+    esz, dt, o = 4, mpi.MPI_FLOAT, mpi.MPI_SUM
+    REF = mpi.MPIX_HIP_ALG_REFERENCE_ORDER
+    comms = mpi.comm_create_loopback(p)
+    try:
+        count = (1 << 21) + 5                      # 8 MiB per rank: blocks >= 1 MiB at p = 8
+        rng = np.random.default_rng(p)
+        xs = [rng.uniform(-1, 1, count).astype(np.float32).view(np.uint8) for _ in range(p)]
+        send = [torch.from_numpy(x.copy()).cuda() for x in xs]
+        recv = [torch.zeros_like(s) for s in send]
+        torch.cuda.synchronize()
+        run_ranks(lambda r: _ok(mpi, mpi.allreduce(send[r].data_ptr(), recv[r].data_ptr(), count, dt, o,
+                                                   comms[r], REF)), p)
+        torch.cuda.synchronize()
+        want = S.allreduce_smp_auto(xs, count, esz, dt, o)
+        for r in range(p):
+            assert np.array_equal(recv[r].cpu().numpy(), want), f"allreduce rank {r}"
+        for root in (0, p - 1):
+            rbuf = torch.zeros_like(send[root])
+            torch.cuda.synchronize()
+            run_ranks(lambda r: _ok(mpi, mpi.reduce(send[r].data_ptr(), rbuf.data_ptr() if r == root else 0,
+                                                    count, dt, o, root, comms[r], REF)), p)
+            torch.cuda.synchronize()
+            assert np.array_equal(rbuf.cpu().numpy(), S.reduce_auto(xs, count, esz, dt, o, root)), f"reduce {root}"
+        rcount = (1 << 18) + 1                     # 1 MiB + 4 B per block: pairwise, skewed slots
+        ys = [rng.uniform(-1, 1, rcount * p).astype(np.float32).view(np.uint8) for _ in range(p)]
+        ysend = [torch.from_numpy(y.copy()).cuda() for y in ys]
+        yrecv = [torch.zeros(rcount * esz, dtype=torch.uint8, device="cuda") for _ in range(p)]
+        torch.cuda.synchronize()
+        run_ranks(lambda r: _ok(mpi, mpi.reduce_scatter_block(ysend[r].data_ptr(), yrecv[r].data_ptr(), rcount, dt,
+                                                              o, comms[r], REF)), p)
+        torch.cuda.synchronize()
+        want = S.reduce_scatter_block_auto(ys, rcount, esz, dt, o)
+        for r in range(p):
+            assert np.array_equal(yrecv[r].cpu().numpy(), want[r]), f"reduce_scatter_block rank {r}"
+        scount = (1 << 18) + 3
+        zs = [rng.uniform(-1, 1, scount).astype(np.float32).view(np.uint8) for _ in range(p)]
+        zsend = [torch.from_numpy(z.copy()).cuda() for z in zs]
+        for fn, sim in ((mpi.scan, S.scan_recursive_doubling), (mpi.exscan, S.exscan_recursive_doubling)):
+            zrecv = [torch.zeros_like(z) for z in zsend]
+            torch.cuda.synchronize()
+            run_ranks(lambda r: _ok(mpi, fn(zsend[r].data_ptr(), zrecv[r].data_ptr(), scount, dt, o, comms[r],
+                                            REF)), p)
+            torch.cuda.synchronize()
+            want = sim(zs, scount, esz, dt, o)
+            for r in range(1 if fn is mpi.exscan else 0, p):
+                assert np.array_equal(zrecv[r].cpu().numpy(), want[r]), f"{fn.__name__} rank {r}"
+    finally:
+        for c in comms:
+            mpi.comm_free(c)

@@ -84,21 +84,19 @@ int main(int argc, char **argv) {
     std::vector<uint32_t> h(bytes / 4);
     uint32_t x = 0x5EED;
     for (auto &v : h) { x ^= x << 13; x ^= x >> 17; x ^= x << 5; v = 0x3c003c00u | (x & 0x03ff03ffu); }  // finite fp16 / fp32
-    for (auto &p : ins) { CK(hipMalloc(&p, bytes)); CK(hipMemcpy(p, h.data(), bytes, hipMemcpyHostToDevice)); }
+    // operand j of set s at base + (s*P + j) * (bytes + skew): skew 0 puts the
+    // eight operands at power-of-two strides (like a staging area of equal blocks)
+    const size_t skew = argc > 3 ? strtoull(argv[3], 0, 10) : 0;
+    char *big;
+    CK(hipMalloc(&big, (bytes + skew) * P * NS + 4096));
+    for (int k = 0; k < P * NS; ++k) {
+        ins[k] = big + (size_t)k * (bytes + skew);
+        CK(hipMemcpy(ins[k], h.data(), bytes, hipMemcpyHostToDevice));
+    }
     for (auto &p : outs) CK(hipMalloc(&p, bytes));
     std::vector<Var> vs = {
         {"TREE8 f32 product", 4, &launch_combine_p<OpSum, float, 8, true>},
-        {"TREE8 f32 U1 T1024 nogap", 4, &launch_mx<float, true, 1, 1024, 0>},
-        {"TREE8 f32 U1 T1024 gap2", 4, &launch_mx<float, true, 1, 1024, 2>},
-        {"TREE8 f32 U1 T1024 gap1", 4, &launch_mx<float, true, 1, 1024, 1>},
-        {"TREE8 f32 U1 T256 gap2", 4, &launch_mx<float, true, 1, 256, 2>},
-        {"TREE8 f32 U2 T256 gap2", 4, &launch_mx<float, true, 2, 256, 2>},
-        {"TREE8 f32 U2 T512 gap2", 4, &launch_mx<float, true, 2, 512, 2>},
-        {"TREE8 f32 U1 T512 gap2", 4, &launch_mx<float, true, 1, 512, 2>},
-        {"TREE8 f32 U1 T1024 gap4", 4, &launch_mx<float, true, 1, 1024, 4>},
         {"CHAIN8 f16 product", 2, &launch_combine_p<OpSum, f16, 8, false>},
-        {"CHAIN8 f16 U1 T1024 gap1", 2, &launch_mx<f16, false, 1, 1024, 1>},
-        {"CHAIN8 f16 U2 T512 gap2", 2, &launch_mx<f16, false, 2, 512, 2>},
     };
     hipStream_t st;
     CK(hipStreamCreate(&st));
@@ -119,6 +117,6 @@ int main(int argc, char **argv) {
             CK(hipStreamSynchronize(st));
         }
     }
-    printf("8 x %zu MiB -> 1, %d rounds; durations: see the rocprofv3 kernel trace\n", mib, rounds);
+    printf("8 x %zu MiB -> 1 (operand stride %zu B), %d rounds; durations: see the rocprofv3 kernel trace\n", mib, bytes + skew, rounds);
     return 0;
 }
