@@ -242,7 +242,10 @@ def main():
 
     # MPI_Reduce_local through the compiled binding (csrc/py/fastcall.c), the
     # way mpi4py calls MPI: ~0.25 us of Python per call instead of ~1.2 us (ctypes)
-    reduce_local = m.fast_reduce_local()
+    try:
+        reduce_local, binding = m.fast_reduce_local(), "compiled CPython binding (csrc/py/fastcall.c)"
+    except ImportError:     # extension not built: the same C entry point through ctypes
+        reduce_local, binding = lib.MPI_Reduce_local, "ctypes"
     dt_f32, op_sum = m.MPI_FLOAT, m.MPI_SUM
 
     def step(i):
@@ -272,7 +275,7 @@ def main():
                         "device-resident, one rank per GPU" % (args.mib, count),
             "count": count,
             "algorithmic_bytes_per_call": alg_bytes,
-            "api": "MPI_Reduce_local (C ABI, synchronous; called through the compiled CPython binding)",
+            "api": "MPI_Reduce_local (C ABI, synchronous; called through the " + binding + ")",
             "parallelism": "replica-per-gpu (no data-path collective)",
         },
         # the synchronous call per GPU (launch + completion included) against the HBM peak
