@@ -11,16 +11,18 @@
 //     is vbytes / 16 KiB workgroups (16384 at 256 MiB), which keeps every CU's
 //     queue deep and the DRAM pages of a tile together;
 //   * all 8 loads of a lane issued before the first combine (latency hiding
-//     by ILP + 8 waves/CU of TLP);
+//     by ILP + 8 waves/CU of TLP), with a one-instruction issue gap after
+//     each (inout, in) pair (issue_gap below: 0.810 -> 0.830-0.841 of peak);
 //   * buffer_load/store_dwordx4 with the `nt` cache policy (aux = 2) on both
 //     operands and on the store: streamed-once data should not displace L2 /
 //     Infinity Cache lines; measured 0.81 of the 8 TB/s HBM peak vs 0.70 for
-//     default-policy loads and 0.63 for a grid-stride loop;
+//     default-policy loads and 0.63 for a grid-stride loop (before the gap);
 //   * the buffer descriptor covers exactly this tile's bytes, so the ragged
 //     last tile needs no branch: out-of-range loads return 0 and out-of-range
 //     stores are dropped by the hardware range check.
 // The < 16 B head (to 16 B-align inout) and tail are handled element-wise by
-// workgroup 0, so a call is always exactly one launch.
+// workgroup 0 (k_reduce_tile), so a call is always exactly one launch; without
+// them the launch takes k_reduce_tile_lean.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
