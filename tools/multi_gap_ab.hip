@@ -60,6 +60,55 @@ __global__ __launch_bounds__(TH) void k_mx(MultiArgs a) {
     }
 }
 
+// issue order test: odd workgroups load the eight operands in reverse order
+template <class T, bool TREE, int TH>
+__global__ __launch_bounds__(TH) void k_rev(MultiArgs a) {
+    constexpr int P = 8;
+    constexpr uint32_t tile = TH * 16;
+    const uint64_t base = (uint64_t)blockIdx.x * tile;
+    if (base >= a.vbytes) return;
+    const uint64_t left = a.vbytes - base;
+    const int nrec = (int)(left < tile ? left : tile);
+    const int t = (int)threadIdx.x;
+    const int off = (t >> 6) * 1024 + (t & 63) * 16;
+    u32x4 x[P];
+    if (blockIdx.x & 1) {
+#pragma unroll
+        for (int j = P - 1; j >= 0; --j) {
+            __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void *)(a.in[j] + base), 0, nrec, 0x00020000);
+            x[j] = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, kCachePolicyNT);
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < P; ++j) {
+            __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void *)(a.in[j] + base), 0, nrec, 0x00020000);
+            x[j] = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, kCachePolicyNT);
+        }
+    }
+    __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc((void *)(a.out + base), 0, nrec, 0x00020000);
+    Pack16<T> pk[P];
+#pragma unroll
+    for (int j = 0; j < P; ++j) pk[j] = __builtin_bit_cast(Pack16<T>, x[j]);
+    Pack16<T> res;
+#pragma unroll
+    for (int k = 0; k < (int)(16 / sizeof(T)); ++k) {
+        T v[P];
+#pragma unroll
+        for (int j = 0; j < P; ++j) v[j] = pk[j].e[k];
+        res.e[k] = fold_fast<OpSum, T, P, TREE>(v);
+    }
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, res), ro, off, 0, kCachePolicyNT);
+}
+template <class T, bool TREE, int TH>
+hipError_t launch_rev(const void *const *ins, void *out, uint64_t count, hipStream_t s) {
+    MultiArgs a{};
+    for (int j = 0; j < 8; ++j) a.in[j] = static_cast<const char *>(ins[j]);
+    a.out = static_cast<char *>(out);
+    a.vbytes = count * sizeof(T);
+    hipLaunchKernelGGL((k_rev<T, TREE, TH>), dim3((unsigned)((a.vbytes + TH * 16 - 1) / (TH * 16))), dim3(TH), 0, s, a);
+    return hipGetLastError();
+}
+
 typedef hipError_t (*mfn)(const void *const *, void *, uint64_t, hipStream_t);
 
 template <class T, bool TREE, int U, int TH, int GAP>
@@ -97,6 +146,8 @@ int main(int argc, char **argv) {
     std::vector<Var> vs = {
         {"TREE8 f32 product", 4, &launch_combine_p<OpSum, float, 8, true>},
         {"CHAIN8 f16 product", 2, &launch_combine_p<OpSum, f16, 8, false>},
+        {"TREE8 f32 odd-reverse", 4, &launch_rev<float, true, 1024>},
+        {"TREE8 f32 wave-layout U1 T1024 gap0", 4, &launch_mx<float, true, 1, 1024, 0>},
     };
     hipStream_t st;
     CK(hipStreamCreate(&st));
