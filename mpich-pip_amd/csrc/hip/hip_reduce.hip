@@ -10,7 +10,10 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
+#include <condition_variable>
 #include <mutex>
+#include <thread>
 
 #include "mpir_hip_reduce.h"
 #include "kernel_table.hpp"
@@ -45,14 +48,16 @@ constexpr int kMaxStageSlots = 8;
 // `stage_slots()` device scratch slots, so host->device and device->host
 // transfers run at the same time (PCIe is full duplex).  Events order the
 // stages of one chunk and stop a slot from being refilled before its
-// copy-back has read it.
+// copy-back has read it.  Defaults 16 MiB x 3 slots (tools/stage_sweep.py,
+// profiles/r01s3_stage_sweep.log: pinned 71.8 GiB/s, pageable 66.3 with the
+// bounce path below; 32 MiB chunks leave a longer tail of copy-outs).
 // MPIR_CVAR_REDUCE_LOCAL_STAGE_CHUNK_MB / MPIR_CVAR_REDUCE_LOCAL_STAGE_SLOTS override.
 // (function-local statics: initialised once, thread-safe)
 uint64_t stage_chunk() {
     static const uint64_t v = [] {
         const char *e = getenv("MPIR_CVAR_REDUCE_LOCAL_STAGE_CHUNK_MB");
         const long mb = e ? atol(e) : 0;
-        return (uint64_t)(mb > 0 && mb <= 1024 ? mb : 32) << 20;
+        return (uint64_t)(mb > 0 && mb <= 1024 ? mb : 16) << 20;
     }();
     return v;
 }
@@ -74,6 +79,8 @@ struct DevCtx {
     uint32_t seq = 0;
     char *scratch = nullptr;     // staging slots x (in, inout) x chunk, or multi-operand temporaries
     size_t scratch_bytes = 0;
+    char *bounce = nullptr;      // pinned host bounce slots x (in, inout) x chunk (pageable operands)
+    size_t bounce_bytes = 0;
 };
 
 struct ThreadCtx {
@@ -165,7 +172,103 @@ int get_scratch(int dev, size_t bytes, char **out) {
     return MPIR_HIP_OK;
 }
 
+int get_bounce(int dev, size_t bytes, char **out) {
+    DevCtx &d = ctx().dev[dev];
+    if (d.bounce_bytes < bytes) {
+        if (d.bounce) HIPCHK(hipDeviceSynchronize());   // in-flight copies may still read it
+        if (d.bounce) HIPCHK(hipHostFree(d.bounce));
+        d.bounce = nullptr;
+        d.bounce_bytes = 0;
+        HIPCHK(hipHostMalloc(&d.bounce, bytes, hipHostMallocDefault));
+        d.bounce_bytes = bytes;
+    }
+    *out = d.bounce;
+    return MPIR_HIP_OK;
+}
+
+// Host copies of the bounce path, split over a small process-wide pool of
+// worker threads: one thread moves 31-33 GB/s between pageable and pinned
+// memory on the MI355X host, four 83-86 GB/s (tools/memcpy_bw.cpp,
+// profiles/r01s3_memcpy_bw.log) -- more than the ~51 GB/s a PCIe Gen5 x16
+// upload takes.  MPIR_CVAR_REDUCE_LOCAL_STAGE_THREADS (default 4; 1 = the
+// calling thread alone).  The pool is never torn down: its idle workers end
+// with the process, so exit never waits on them.
+class CopyPool {
+  public:
+    explicit CopyPool(int nthreads) : n_(nthreads) {
+        for (int i = 1; i < n_; ++i) std::thread([this] { work(); }).detach();
+    }
+    void copy(char *dst, const char *src, size_t bytes) {
+        if (n_ <= 1 || bytes < ((size_t)1 << 20)) {
+            memcpy(dst, src, bytes);
+            return;
+        }
+        std::lock_guard<std::mutex> job(job_mu_);       // one split copy at a time
+        const size_t part = ((bytes + n_ - 1) / n_ + 63) & ~(size_t)63;
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            dst_ = dst;
+            src_ = src;
+            bytes_ = bytes;
+            part_ = part;
+            next_ = 1;                                  // part 0 is the caller's
+            pending_ = (bytes + part - 1) / part - 1;
+            ++gen_;
+        }
+        cv_.notify_all();
+        memcpy(dst, src, std::min(part, bytes));
+        std::unique_lock<std::mutex> lk(mu_);
+        done_.wait(lk, [this] { return pending_ == 0; });
+    }
+
+  private:
+    void work() {
+        uint64_t seen = 0;
+        std::unique_lock<std::mutex> lk(mu_);
+        for (;;) {
+            cv_.wait(lk, [&] { return gen_ != seen; });
+            seen = gen_;
+            while (next_ * part_ < bytes_) {
+                const size_t k = next_++;
+                char *d = dst_ + k * part_;
+                const char *sp = src_ + k * part_;
+                const size_t nb = std::min(part_, bytes_ - k * part_);
+                lk.unlock();
+                memcpy(d, sp, nb);
+                lk.lock();
+                if (--pending_ == 0) done_.notify_one();
+            }
+        }
+    }
+    int n_;
+    std::mutex job_mu_, mu_;
+    std::condition_variable cv_, done_;
+    char *dst_ = nullptr;
+    const char *src_ = nullptr;
+    size_t bytes_ = 0, part_ = 1, next_ = 0, pending_ = 0;
+    uint64_t gen_ = 0;
+};
+
+CopyPool &copy_pool() {
+    static CopyPool *pool = [] {
+        const char *e = getenv("MPIR_CVAR_REDUCE_LOCAL_STAGE_THREADS");
+        const int n = e ? atoi(e) : 4;
+        return new CopyPool(n >= 1 && n <= 64 ? n : 4);
+    }();
+    return *pool;
+}
+
 enum Loc { LOC_HOST = 0, LOC_DEVICE = 1 };
+
+// page-locked host memory (hipHostMalloc / hipHostRegister): DMA-able as is
+bool is_pinned_host(const void *p) {
+    hipPointerAttribute_t at;
+    if (hipPointerGetAttributes(&at, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return at.type == hipMemoryTypeHost;
+}
 
 // Device memory (hipMalloc, managed) is combined in place; anything else
 // (pageable or pinned host memory) is staged through device scratch.
@@ -393,31 +496,67 @@ int MPIR_Hip_reduce(const void *inbuf, void *inoutbuf, uint64_t count, int op, i
     if (rc == MPIR_HIP_OK) rc = get_stage_events(dev, nslots);
     const char *cin = static_cast<const char *>(inbuf);
     char *cio = static_cast<char *>(inoutbuf);
+    // Pageable host operands go through pinned bounce slots that the copy pool
+    // fills and drains while the GPU works on earlier chunks (HIP's own
+    // pageable path uploads ~36 GB/s; pinned memory is DMA'd directly).
+    const bool bounce_in = stage_in && lin == LOC_HOST && !is_pinned_host(inbuf);
+    const bool bounce_io = stage_io && lio == LOC_HOST && !is_pinned_host(inoutbuf);
+    char *bounce = nullptr;
+    if (rc == MPIR_HIP_OK && (bounce_in || bounce_io))
+        rc = get_bounce(dev, (size_t)(2 * nslots) * slot_bytes, &bounce);
+    CopyPool &pool = copy_pool();
+    const uint64_t nchunks = (total + chunk_bytes - 1) / chunk_bytes;
+    // chunk j's result: from its bounce slot to the caller's inoutbuf, once its
+    // copy-back (recorded as ev_free of its slot) has landed
+    auto drain = [&](uint64_t j) -> int {
+        const int sl = (int)(j % (uint64_t)nslots);
+        const uint64_t o = j * chunk_bytes, n = (total - o < chunk_bytes) ? total - o : chunk_bytes;
+        hipError_t e = hipEventSynchronize(d.ev_free[sl]);
+        if (e != hipSuccess) return set_err(e, "staged reduce");
+        pool.copy(cio + o, bounce + (2 * sl + 1) * slot_bytes, n);
+        return MPIR_HIP_OK;
+    };
     for (uint64_t off = 0, k = 0; rc == MPIR_HIP_OK && off < total; off += chunk_bytes, ++k) {
         const uint64_t nb = (total - off < chunk_bytes) ? total - off : chunk_bytes;
         const int slot = (int)(k % (uint64_t)nslots);
         char *sin = scratch + (2 * slot) * slot_bytes;
         char *sio = scratch + (2 * slot + 1) * slot_bytes;
+        char *bin = bounce ? bounce + (2 * slot) * slot_bytes : nullptr;
+        char *bio = bounce ? bounce + (2 * slot + 1) * slot_bytes : nullptr;
         const void *kin = stage_in ? (const void *)sin : (const void *)(cin + off);
         void *kio = stage_io ? (void *)sio : (void *)(cio + off);
         hipError_t e = hipSuccess;
         // the slot's previous chunk must be fully consumed (kernel read, copy-back done)
-        if (k >= (uint64_t)nslots) e = hipStreamWaitEvent(up, d.ev_free[slot], 0);
-        if (e == hipSuccess && stage_in) e = hipMemcpyAsync(sin, cin + off, nb, hipMemcpyDefault, up);
-        if (e == hipSuccess && stage_io) e = hipMemcpyAsync(sio, cio + off, nb, hipMemcpyDefault, up);
+        if (k >= (uint64_t)nslots) {
+            if (bounce_io) {
+                if ((rc = drain(k - nslots)) != MPIR_HIP_OK) break;
+            } else if (bounce_in) {
+                e = hipEventSynchronize(d.ev_free[slot]);   // the host rewrites bin
+            }
+            if (e == hipSuccess) e = hipStreamWaitEvent(up, d.ev_free[slot], 0);
+        }
+        if (e == hipSuccess && bounce_in) pool.copy(bin, cin + off, nb);
+        if (e == hipSuccess && bounce_io) pool.copy(bio, cio + off, nb);
+        if (e == hipSuccess && stage_in)
+            e = hipMemcpyAsync(sin, bounce_in ? (const void *)bin : (const void *)(cin + off), nb, hipMemcpyDefault, up);
+        if (e == hipSuccess && stage_io)
+            e = hipMemcpyAsync(sio, bounce_io ? (const void *)bio : (const void *)(cio + off), nb, hipMemcpyDefault, up);
         if (e == hipSuccess) e = hipEventRecord(d.ev_up[slot], up);
         if (e == hipSuccess) e = hipStreamWaitEvent(comp, d.ev_up[slot], 0);
         if (e == hipSuccess) e = fn(kin, kio, nb / unit, comp);
         if (e == hipSuccess) e = hipEventRecord(d.ev_comp[slot], comp);
         if (stage_io) {
             if (e == hipSuccess) e = hipStreamWaitEvent(down, d.ev_comp[slot], 0);
-            if (e == hipSuccess) e = hipMemcpyAsync(cio + off, sio, nb, hipMemcpyDefault, down);
+            if (e == hipSuccess) e = hipMemcpyAsync(bounce_io ? (void *)bio : (void *)(cio + off), sio, nb, hipMemcpyDefault, down);
             if (e == hipSuccess) e = hipEventRecord(d.ev_free[slot], down);
         } else if (e == hipSuccess) {
             e = hipEventRecord(d.ev_free[slot], comp);
         }
         if (e != hipSuccess) rc = set_err(e, "staged reduce");
     }
+    if (rc == MPIR_HIP_OK && bounce_io)
+        for (uint64_t j = nchunks > (uint64_t)nslots ? nchunks - nslots : 0; rc == MPIR_HIP_OK && j < nchunks; ++j)
+            rc = drain(j);
     if (rc == MPIR_HIP_OK) rc = wait_stream_block(comp);
     if (rc == MPIR_HIP_OK) rc = wait_stream_block(down);
     if (cur != dev) (void)hipSetDevice(cur);

@@ -164,12 +164,16 @@ def test_survey_probes_on_gpu(mpi, cuda):
         assert [int(x) for x in got] == c["expect"], c["id"]
 
 
-@pytest.mark.parametrize("where", ["host-host", "host-dev", "dev-host", "pinned-pinned", "pinned-dev"])
+@pytest.mark.parametrize("where", ["host-host", "host-dev", "dev-host", "pinned-pinned", "pinned-dev",
+                                   "host-pinned", "pinned-host", "hostoff-hostoff"])
 def test_host_and_mixed_pointers(mpi, orc, cuda, where):
-    """Rank buffers that arrive in host memory (PiP shm) are staged through the GPU."""
+    """Rank buffers that arrive in host memory (PiP shm) are staged through the GPU:
+    pageable operands through the pinned bounce slots (several chunks per call at
+    the 192 MiB size, so slots are reused), pinned ones DMA'd directly; `hostoff`
+    is a pageable buffer 4 bytes past 64 B alignment."""
     torch = cuda
     for n, t, op in ((1000, "MPI_FLOAT", "MPI_SUM"), (3 * (16 << 20) + 5, "MPI_INT", "MPI_MAX"),
-                     (777, "MPI_DOUBLE_INT", "MPI_MINLOC")):
+                     (777, "MPI_DOUBLE_INT", "MPI_MINLOC"), ((9 << 20) + 3, "MPI_DOUBLE", "MPI_SUM")):
         rng = np.random.default_rng(n)
         a = T.to_bytes(T.gen(t, n, rng, op))
         b = T.to_bytes(T.gen(t, n, rng, op))
@@ -184,6 +188,12 @@ def test_host_and_mixed_pointers(mpi, orc, cuda, where):
             if kind == "pinned":
                 tt = torch.from_numpy(x.copy()).pin_memory()
                 return tt, tt.data_ptr()
+            if kind == "hostoff":
+                raw = np.zeros(x.size + 64 + 4, np.uint8)
+                o = (-raw.ctypes.data) % 64 + 4
+                h = raw[o:o + x.size]
+                h[:] = x
+                return h, h.ctypes.data
             h = x.copy()
             return h, h.ctypes.data
 
