@@ -504,7 +504,7 @@ int MPIR_Hip_reduce(const void *inbuf, void *inoutbuf, uint64_t count, int op, i
     char *bounce = nullptr;
     if (rc == MPIR_HIP_OK && (bounce_in || bounce_io))
         rc = get_bounce(dev, (size_t)(2 * nslots) * slot_bytes, &bounce);
-    CopyPool &pool = copy_pool();
+    CopyPool *pool = (bounce_in || bounce_io) ? &copy_pool() : nullptr;   // threads only when needed
     const uint64_t nchunks = (total + chunk_bytes - 1) / chunk_bytes;
     // chunk j's result: from its bounce slot to the caller's inoutbuf, once its
     // copy-back (recorded as ev_free of its slot) has landed
@@ -513,7 +513,7 @@ int MPIR_Hip_reduce(const void *inbuf, void *inoutbuf, uint64_t count, int op, i
         const uint64_t o = j * chunk_bytes, n = (total - o < chunk_bytes) ? total - o : chunk_bytes;
         hipError_t e = hipEventSynchronize(d.ev_free[sl]);
         if (e != hipSuccess) return set_err(e, "staged reduce");
-        pool.copy(cio + o, bounce + (2 * sl + 1) * slot_bytes, n);
+        pool->copy(cio + o, bounce + (2 * sl + 1) * slot_bytes, n);
         return MPIR_HIP_OK;
     };
     for (uint64_t off = 0, k = 0; rc == MPIR_HIP_OK && off < total; off += chunk_bytes, ++k) {
@@ -535,8 +535,8 @@ int MPIR_Hip_reduce(const void *inbuf, void *inoutbuf, uint64_t count, int op, i
             }
             if (e == hipSuccess) e = hipStreamWaitEvent(up, d.ev_free[slot], 0);
         }
-        if (e == hipSuccess && bounce_in) pool.copy(bin, cin + off, nb);
-        if (e == hipSuccess && bounce_io) pool.copy(bio, cio + off, nb);
+        if (e == hipSuccess && bounce_in) pool->copy(bin, cin + off, nb);
+        if (e == hipSuccess && bounce_io) pool->copy(bio, cio + off, nb);
         if (e == hipSuccess && stage_in)
             e = hipMemcpyAsync(sin, bounce_in ? (const void *)bin : (const void *)(cin + off), nb, hipMemcpyDefault, up);
         if (e == hipSuccess && stage_io)
