@@ -477,16 +477,21 @@ __global__ __launch_bounds__(TH) void k_combine_multi(MultiArgs a) {
     if (base < a.vbytes) {
         const uint64_t left = a.vbytes - base;
         const int nrec = (int)(left < tile ? left : tile);
+        // each wave owns a contiguous U KiB of every operand's tile (as in the
+        // two-operand kernel); the loads go vector by vector across the P
+        // operands with an issue gap after every (P == 2 ? 2 : 4) of them
+        const int t = (int)threadIdx.x;
+        const int wb = (t >> 6) * (U * 1024) + (t & 63) * 16;
+        constexpr int GAP = P == 2 ? 2 : 4;
         u32x4 x[P][U];
 #pragma unroll
-        for (int j = 0; j < P; ++j) {
-            __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void *)(a.in[j] + base), 0, nrec, 0x00020000);
+        for (int u = 0; u < U; ++u)
 #pragma unroll
-            for (int u = 0; u < U; ++u) {
-                x[j][u] = __builtin_amdgcn_raw_buffer_load_b128(r, (u * TH + (int)threadIdx.x) * 16, 0, kCachePolicyNT);
-                if (((j * U + u) & 1) && j * U + u + 1 < P * U) issue_gap();
+            for (int j = 0; j < P; ++j) {
+                __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void *)(a.in[j] + base), 0, nrec, 0x00020000);
+                x[j][u] = __builtin_amdgcn_raw_buffer_load_b128(r, wb + u * 1024, 0, kCachePolicyNT);
+                if ((u * P + j + 1) % GAP == 0 && u * P + j + 1 < U * P) issue_gap();
             }
-        }
         __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc((void *)(a.out + base), 0, nrec, 0x00020000);
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -501,8 +506,7 @@ __global__ __launch_bounds__(TH) void k_combine_multi(MultiArgs a) {
                 for (int j = 0; j < P; ++j) v[j] = pk[j].e[k];
                 res.e[k] = fold_fast<Op, T, P, TREE>(v);
             }
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, res), ro,
-                                                   (u * TH + (int)threadIdx.x) * 16, 0, kCachePolicyNT);
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, res), ro, wb + u * 1024, 0, kCachePolicyNT);
         }
     }
     if (blockIdx.x == 0) {
@@ -642,7 +646,10 @@ hipError_t launch_combine_any(const void *const *ins, int n, int tree, void *out
 
 template <class Op, class T, int P, bool TREE>
 hipError_t launch_combine_p(const void *const *ins, void *out_, uint64_t count, hipStream_t s) {
-    return launch_combine_pu<Op, T, P, TREE, (P >= 8 ? 1 : (P >= 4 ? 2 : 4)), (P >= 8 ? 1024 : kThreads)>(ins, out_, count, s);
+    // rocprofv3 trace, 32 MiB blocks (profiles/r01s3_multi_shape_p24.log): P = 8 on
+    // 1024-thread WGs (0.76-0.80 of peak); P = 4 with 4 vectors per lane 0.78-0.80
+    // (2 vectors: 0.72-0.74); P = 2 with 4 vectors per lane 0.74-0.76
+    return launch_combine_pu<Op, T, P, TREE, (P >= 8 ? 1 : 4), (P >= 8 ? 1024 : kThreads)>(ins, out_, count, s);
 }
 
 }  // namespace mpir_hip

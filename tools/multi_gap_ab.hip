@@ -111,14 +111,14 @@ hipError_t launch_rev(const void *const *ins, void *out, uint64_t count, hipStre
 
 typedef hipError_t (*mfn)(const void *const *, void *, uint64_t, hipStream_t);
 
-template <class T, bool TREE, int U, int TH, int GAP>
+template <class T, bool TREE, int U, int TH, int GAP, int P = 8>
 hipError_t launch_mx(const void *const *ins, void *out, uint64_t count, hipStream_t s) {
     MultiArgs a{};
-    for (int j = 0; j < 8; ++j) a.in[j] = static_cast<const char *>(ins[j]);
+    for (int j = 0; j < P; ++j) a.in[j] = static_cast<const char *>(ins[j]);
     a.out = static_cast<char *>(out);
     a.vbytes = count * sizeof(T);
     constexpr uint32_t tile = TH * U * 16;
-    hipLaunchKernelGGL((k_mx<T, TREE, 8, U, TH, GAP>), dim3((unsigned)((a.vbytes + tile - 1) / tile)), dim3(TH), 0, s, a);
+    hipLaunchKernelGGL((k_mx<T, TREE, P, U, TH, GAP>), dim3((unsigned)((a.vbytes + tile - 1) / tile)), dim3(TH), 0, s, a);
     return hipGetLastError();
 }
 
@@ -143,11 +143,16 @@ int main(int argc, char **argv) {
         CK(hipMemcpy(ins[k], h.data(), bytes, hipMemcpyHostToDevice));
     }
     for (auto &p : outs) CK(hipMalloc(&p, bytes));
+    // P = 2 / 4 shapes (the first P operands of a set); algorithmic bytes (P+1) x block
     std::vector<Var> vs = {
-        {"TREE8 f32 product", 4, &launch_combine_p<OpSum, float, 8, true>},
-        {"CHAIN8 f16 product", 2, &launch_combine_p<OpSum, f16, 8, false>},
-        {"TREE8 f32 odd-reverse", 4, &launch_rev<float, true, 1024>},
-        {"TREE8 f32 wave-layout U1 T1024 gap0", 4, &launch_mx<float, true, 1, 1024, 0>},
+        {"TREE2 f32 product (U4 T256)", 4, &launch_combine_p<OpSum, float, 2, true>},
+        {"TREE2 f32 U4 T256 gap2", 4, &launch_mx<float, true, 4, 256, 2, 2>},
+        {"TREE2 f32 U2 T512 gap2", 4, &launch_mx<float, true, 2, 512, 2, 2>},
+        {"TREE2 f32 U1 T1024 gap0", 4, &launch_mx<float, true, 1, 1024, 0, 2>},
+        {"TREE4 f32 product (U2 T256)", 4, &launch_combine_p<OpSum, float, 4, true>},
+        {"TREE4 f32 U2 T512 gap2", 4, &launch_mx<float, true, 2, 512, 2, 4>},
+        {"TREE4 f32 U1 T1024 gap2", 4, &launch_mx<float, true, 1, 1024, 2, 4>},
+        {"TREE4 f32 U4 T256 gap4", 4, &launch_mx<float, true, 4, 256, 4, 4>},
     };
     hipStream_t st;
     CK(hipStreamCreate(&st));
