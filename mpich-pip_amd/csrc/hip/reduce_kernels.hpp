@@ -200,10 +200,12 @@ __global__ __launch_bounds__(kThreads) void k_reduce_shift(ShiftArgs<T> args) {
         __amdgpu_buffer_rsrc_t rin = __builtin_amdgcn_make_buffer_rsrc((void *)(args.in_al + base), 0, nrec_in, 0x00020000);
         __amdgpu_buffer_rsrc_t rio = __builtin_amdgcn_make_buffer_rsrc((void *)(ta.io + base), 0, nrec, 0x00020000);
         const bool last_lane = (threadIdx.x & 63) == 63;
+        // wave-contiguous 4 KiB per wave, as in the aligned tile kernel
+        const int wb = ((int)threadIdx.x >> 6) * (kVecPerLane * 1024) + ((int)threadIdx.x & 63) * 16;
         u32x4 a[kVecPerLane], b[kVecPerLane], n63[kVecPerLane];
 #pragma unroll
         for (int u = 0; u < kVecPerLane; ++u) {
-            const int off = (u * kThreads + (int)threadIdx.x) * 16;
+            const int off = wb + u * 1024;
             a[u] = __builtin_amdgcn_raw_buffer_load_b128(rio, off, 0, kCachePolicyNT);
             b[u] = __builtin_amdgcn_raw_buffer_load_b128(rin, off, 0, kCachePolicyNT);
             // lane 63's neighbour vector: every lane issues the load, the others
@@ -214,7 +216,7 @@ __global__ __launch_bounds__(kThreads) void k_reduce_shift(ShiftArgs<T> args) {
         }
 #pragma unroll
         for (int u = 0; u < kVecPerLane; ++u) {
-            const int off = (u * kThreads + (int)threadIdx.x) * 16;
+            const int off = wb + u * 1024;
             // neighbour from the shuffle, OR the lane-63 load (0 on every other
             // lane): branch-free, so the load cannot be sunk into a branch
             const uint32_t keep = last_lane ? 0u : ~0u;
@@ -352,17 +354,20 @@ __global__ __launch_bounds__(kThreads) void k_reduce_tile_wide(const char *in, c
     __amdgpu_buffer_rsrc_t rin = __builtin_amdgcn_make_buffer_rsrc((void *)(in + base), 0, nrec, 0x00020000);
     __amdgpu_buffer_rsrc_t rio = __builtin_amdgcn_make_buffer_rsrc((void *)(io + base), 0, nrec, 0x00020000);
     const int t = (int)threadIdx.x;
+    // each wave owns a contiguous NV KiB of the tile; LDS slot = byte offset / 16,
+    // so element e still sits in slots 2e, 2e+1 whichever lane loaded it
+    const int wv = (t >> 6) * NV * 64 + (t & 63);    // 16-byte vector index of v = 0
     u32x4 a[NV], b[NV];
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
-        a[v] = __builtin_amdgcn_raw_buffer_load_b128(rio, (v * kThreads + t) * 16, 0, kCachePolicyNT);
-        b[v] = __builtin_amdgcn_raw_buffer_load_b128(rin, (v * kThreads + t) * 16, 0, kCachePolicyNT);
+        a[v] = __builtin_amdgcn_raw_buffer_load_b128(rio, (wv + v * 64) * 16, 0, kCachePolicyNT);
+        b[v] = __builtin_amdgcn_raw_buffer_load_b128(rin, (wv + v * 64) * 16, 0, kCachePolicyNT);
         if (v + 1 < NV) issue_gap();
     }
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
-        sa[v * kThreads + t] = a[v];
-        sb[v * kThreads + t] = b[v];
+        sa[wv + v * 64] = a[v];
+        sb[wv + v * 64] = b[v];
     }
     __syncthreads();
     Op op;
@@ -379,7 +384,7 @@ __global__ __launch_bounds__(kThreads) void k_reduce_tile_wide(const char *in, c
     __syncthreads();
 #pragma unroll
     for (int v = 0; v < NV; ++v)
-        __builtin_amdgcn_raw_buffer_store_b128(sa[v * kThreads + t], rio, (v * kThreads + t) * 16, 0, kCachePolicyNT);
+        __builtin_amdgcn_raw_buffer_store_b128(sa[wv + v * 64], rio, (wv + v * 64) * 16, 0, kCachePolicyNT);
 }
 
 // EPL: elements per lane (2 for the memory-bound ops; the compute-bound soft
