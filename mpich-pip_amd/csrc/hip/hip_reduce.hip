@@ -9,6 +9,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <condition_variable>
@@ -195,11 +196,12 @@ int get_bounce(int dev, size_t bytes, char **out) {
 // with the process, so exit never waits on them.
 class CopyPool {
   public:
-    explicit CopyPool(int nthreads) : n_(nthreads) {
+    explicit CopyPool(int nthreads) : n_(nthreads), pid_(getpid()) {
         for (int i = 1; i < n_; ++i) std::thread([this] { work(); }).detach();
     }
     void copy(char *dst, const char *src, size_t bytes) {
-        if (n_ <= 1 || bytes < ((size_t)1 << 20)) {
+        // a forked child has none of the workers: copy alone there
+        if (n_ <= 1 || bytes < ((size_t)1 << 20) || getpid() != pid_) {
             memcpy(dst, src, bytes);
             return;
         }
@@ -241,6 +243,7 @@ class CopyPool {
         }
     }
     int n_;
+    pid_t pid_;
     std::mutex job_mu_, mu_;
     std::condition_variable cv_, done_;
     char *dst_ = nullptr;
