@@ -508,3 +508,39 @@ def test_thread_contexts_reused(mpi, cuda):
     assert not errs
     assert mpi.load().MPIR_Hip_thread_contexts() - before <= 4
     assert torch.equal(x, torch.arange(n, dtype=torch.int64, device="cuda") + 65)
+
+
+def test_concurrent_pageable_threads(mpi, orc, cuda):
+    """Four host threads reduce pageable host buffers at once: each has its own
+    staging streams and bounce slots, and they share the copy pool (one split
+    copy at a time); every result bit-exact."""
+    import threading
+    n = (10 << 20) + 17                      # 40 MiB of fp32: several 16 MiB chunks per call
+    rng = np.random.default_rng(9)
+    data = []
+    for i in range(4):
+        a = rng.uniform(-1, 1, n).astype(np.float32)
+        b = rng.uniform(-1, 1, n).astype(np.float32)
+        data.append((a, b, a + b, a.copy()))  # one IEEE add per element, as the reference
+    errs = []
+
+    def work(i):
+        a, b, _, a0 = data[i]
+        for rep in range(2):
+            if i % 2:
+                rc = mpi.reduce_local(b.ctypes.data, a.ctypes.data, n, mpi.MPI_FLOAT, mpi.MPI_SUM)
+            else:
+                rc = mpi.fast_reduce_local()(b.ctypes.data, a.ctypes.data, n, mpi.MPI_FLOAT, mpi.MPI_SUM)
+            if rc:
+                errs.append((i, rc))
+            if rep == 0:
+                np.copyto(a, a0)                # restore: the second call recomputes the same sum
+
+    ths = [threading.Thread(target=work, args=(i,)) for i in range(4)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join(120)
+    assert not errs
+    for a, b, want, _ in data:
+        assert np.array_equal(a, want)
