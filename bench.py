@@ -380,6 +380,18 @@ def main():
                 "per_core": round(cv / threads, 2),
                 "seconds": round(secs, 3),
             }
+            # the same loop built with clang -O2 (SURVEY.md §8d asks for both compilers)
+            cerr = "thread failure"
+            try:
+                csecs = oracle.cpu_baseline_sum_f32(threads, count, args.cpu_iters, "clang")
+            except RuntimeError as e:
+                csecs, cerr = -1.0, str(e)
+            if csecs > 0:
+                ccv = alg_bytes * args.cpu_iters * threads / csecs / GIB
+                out["cpu_baseline"]["clang_O2"] = {"value": round(ccv, 2), "per_core": round(ccv / threads, 2),
+                                                   "seconds": round(csecs, 3)}
+            else:
+                out["cpu_baseline"]["clang_O2"] = {"error": cerr}
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

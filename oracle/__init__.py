@@ -11,24 +11,40 @@ import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "liboracle.so")
+CLANG_LIB_PATH = os.path.join(HERE, "liboracle_clang.so")   # same sources, clang -O2 (CPU baseline only)
 _lib = None
+_clang = None
+
+
+def _open(path: str) -> ctypes.CDLL:
+    if not os.path.exists(path):
+        raise RuntimeError(f"{path} missing: run `make -C oracle`")
+    lib = ctypes.CDLL(path)
+    vp, i32 = ctypes.c_void_p, ctypes.c_int
+    for name in ("oracle_reduce_local", "oracle_reduce_local_nocheck"):
+        f = getattr(lib, name)
+        f.argtypes = [vp, vp, i32, i32, i32]
+        f.restype = i32
+    lib.oracle_cpu_baseline_sum_f32.argtypes = [i32, ctypes.c_long, i32]
+    lib.oracle_cpu_baseline_sum_f32.restype = ctypes.c_double
+    return lib
+
+
+def load_clang() -> ctypes.CDLL:
+    """The clang -O2 build of the same sources: a second CPU baseline, never the checker."""
+    global _clang
+    if _clang is None:
+        _clang = _open(CLANG_LIB_PATH)
+    return _clang
 
 
 def load() -> ctypes.CDLL:
     global _lib
     if _lib is None:
-        if not os.path.exists(LIB_PATH):
-            raise RuntimeError(f"{LIB_PATH} missing: run `make -C oracle`")
-        lib = ctypes.CDLL(LIB_PATH)
-        vp, i32 = ctypes.c_void_p, ctypes.c_int
-        for name in ("oracle_reduce_local", "oracle_reduce_local_nocheck"):
-            f = getattr(lib, name)
-            f.argtypes = [vp, vp, i32, i32, i32]
-            f.restype = i32
+        lib = _open(LIB_PATH)
+        i32 = ctypes.c_int
         lib.oracle_check_dtype.argtypes = [i32, i32]
         lib.oracle_check_dtype.restype = i32
-        lib.oracle_cpu_baseline_sum_f32.argtypes = [i32, ctypes.c_long, i32]
-        lib.oracle_cpu_baseline_sum_f32.restype = ctypes.c_double
         lib.oracle_h2f.argtypes = [ctypes.c_uint16]
         lib.oracle_h2f.restype = ctypes.c_float
         lib.oracle_f2h.argtypes = [ctypes.c_float]
@@ -50,6 +66,8 @@ def check_dtype(op: int, datatype: int) -> int:
     return load().oracle_check_dtype(op, datatype)
 
 
-def cpu_baseline_sum_f32(nthreads: int, count: int, iters: int) -> float:
-    """Seconds taken by the slowest of `nthreads` threads doing `iters` fp32 SUM calls of `count`."""
-    return load().oracle_cpu_baseline_sum_f32(nthreads, count, iters)
+def cpu_baseline_sum_f32(nthreads: int, count: int, iters: int, compiler: str = "gcc") -> float:
+    """Seconds taken by the slowest of `nthreads` threads doing `iters` fp32 SUM calls of `count`
+    (compiler "gcc": liboracle.so, MPICH's default build; "clang": liboracle_clang.so)."""
+    lib = load_clang() if compiler == "clang" else load()
+    return lib.oracle_cpu_baseline_sum_f32(nthreads, count, iters)
