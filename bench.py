@@ -199,6 +199,20 @@ def load_traffic(count_bytes: int):
     return d.get("hbm_bytes_per_launch"), os.path.relpath(p, ROOT)
 
 
+def host_cpu(affinity: int) -> str:
+    """CPU model and the core counts the baseline ran beside (record nproc/lscpu)."""
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for ln in f:
+                if ln.startswith("model name"):
+                    model = ln.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return f"{model}; {os.cpu_count()} logical CPUs on the host, {affinity} in this process's affinity"
+
+
 def main():
     args = parse()
     import torch
@@ -379,6 +393,7 @@ def main():
                           f"{args.mib} MiB fp32 (inbuf, inoutbuf) pair; oracle/op_oracle.c SUM loop, gcc -O2",
                 "per_core": round(cv / threads, 2),
                 "seconds": round(secs, 3),
+                "host": host_cpu(aff),
             }
             # the same loop built with clang -O2 (SURVEY.md §8d asks for both compilers)
             cerr = "thread failure"
