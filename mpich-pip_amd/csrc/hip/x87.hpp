@@ -137,19 +137,9 @@ X87_FN int x80_uexp(const x80 &v) {
     return (e == 0 ? 1 : e) - 16383;
 }
 
-// result = a + b (sub: a - b); the pad bytes of the result are `pad`'s
-X87_FN x80 x80_addsub(x80 a, x80 b, bool sub, const x80 &pad) {
-    const int ca = x80_class(a), cb = x80_class(b);
-    if (ca == X80_INVALID || cb == X80_INVALID) return x80_indefinite(pad);
-    if (x80_is_nan_class(ca) || x80_is_nan_class(cb)) return x80_nan_result(a, b, ca, cb, pad);
-    uint32_t sa = a.se >> 15, sb = (b.se >> 15) ^ (sub ? 1u : 0u);
-    if (ca == X80_INF || cb == X80_INF) {
-        if (ca == X80_INF && cb == X80_INF && sa != sb) return x80_indefinite(pad);
-        return x80_make(ca == X80_INF ? sa : sb, 0x7fff, 1ull << 63, pad);
-    }
-    if (ca == X80_ZERO && cb == X80_ZERO) return x80_make(sa & sb, 0, 0, pad);
-    int ea = ca == X80_ZERO ? -100000 : x80_uexp(a), eb = cb == X80_ZERO ? -100000 : x80_uexp(b);
-    uint64_t ma = a.m, mb = b.m;
+// finite, not both zero: sign, unbiased exponent (-100000 for a zero) and
+// significand of each operand (the sign of b already flipped for a subtraction)
+X87_FN x80 x80_addsub_core(uint32_t sa, uint32_t sb, int ea, int eb, uint64_t ma, uint64_t mb, const x80 &pad) {
     // order by magnitude: |a| >= |b|
     if (eb > ea || (eb == ea && mb > ma)) {
         int te = ea; ea = eb; eb = te;
@@ -196,6 +186,28 @@ X87_FN x80 x80_addsub(x80 a, x80 b, bool sub, const x80 &pad) {
     return x80_round_pack(sa, ea - 126, s, pad);
 }
 
+
+// result = a + b (sub: a - b); the pad bytes of the result are `pad`'s
+X87_FN x80 x80_addsub(x80 a, x80 b, bool sub, const x80 &pad) {
+    const int ca = x80_class(a), cb = x80_class(b);
+    if (ca == X80_INVALID || cb == X80_INVALID) return x80_indefinite(pad);
+    if (x80_is_nan_class(ca) || x80_is_nan_class(cb)) return x80_nan_result(a, b, ca, cb, pad);
+    uint32_t sa = a.se >> 15, sb = (b.se >> 15) ^ (sub ? 1u : 0u);
+    if (ca == X80_INF || cb == X80_INF) {
+        if (ca == X80_INF && cb == X80_INF && sa != sb) return x80_indefinite(pad);
+        return x80_make(ca == X80_INF ? sa : sb, 0x7fff, 1ull << 63, pad);
+    }
+    if (ca == X80_ZERO && cb == X80_ZERO) return x80_make(sa & sb, 0, 0, pad);
+    const int ea = ca == X80_ZERO ? -100000 : x80_uexp(a), eb = cb == X80_ZERO ? -100000 : x80_uexp(b);
+    return x80_addsub_core(sa, sb, ea, eb, a.m, b.m, pad);
+}
+
+// a + b (sub: a - b) of two NORMAL values (integer bit set, exponent field
+// 1..32766): x80_addsub without the class checks, which cannot fire
+X87_FN x80 x80_addsub_normal(const x80 &a, const x80 &b, bool sub, const x80 &pad) {
+    return x80_addsub_core(a.se >> 15, (b.se >> 15) ^ (sub ? 1u : 0u), (int)(a.se & 0x7fff) - 16383,
+                           (int)(b.se & 0x7fff) - 16383, a.m, b.m, pad);
+}
 X87_FN x80 x80_add(x80 a, x80 b, const x80 &pad) { return x80_addsub(a, b, false, pad); }
 X87_FN x80 x80_sub(x80 a, x80 b, const x80 &pad) { return x80_addsub(a, b, true, pad); }
 
@@ -277,10 +289,43 @@ X87_FN x80 x80_signed_const(int one, const x80 &v, const x80 &pad) {
 X87_FN x80 x80_one(const x80 &pad) { return x80_make(0, 0x3fff, 1ull << 63, pad); }
 X87_FN x80 x80_zero(const x80 &pad) { return x80_make(0, 0, 0, pad); }
 
+// Product of two normal values whose biased exponents both lie in
+// [kX80SafeLo, kX80SafeHi]: the result is normal and finite (its biased
+// exponent stays within [17, 32739] even after a rounding carry), so no class
+// checks and no general rounder; same rounding as x80_mul's normal path.
+constexpr int kX80SafeLo = 8200, kX80SafeHi = 24560;
+X87_FN x80 x80_mul_safe(const x80 &a, const x80 &b, const x80 &pad) {
+    const uint32_t s = (a.se >> 15) ^ (b.se >> 15);
+    const u128 prod = (u128)a.m * (u128)b.m;
+    const uint64_t hi = (uint64_t)(prod >> 64), lo = (uint64_t)prod;
+    const bool top = (hi >> 63) != 0;
+    int er = (int)(a.se & 0x7fff) + (int)(b.se & 0x7fff) - 16383 + (top ? 1 : 0);
+    uint64_t sig, rem, half;
+    if (top) { sig = hi; rem = lo; half = 1ull << 63; }
+    else { sig = (hi << 1) | (lo >> 63); rem = lo & ~(1ull << 63); half = 1ull << 62; }
+    if (rem > half || (rem == half && (sig & 1))) {
+        if (++sig == 0) { sig = 1ull << 63; ++er; }
+    }
+    return x80_make(s, (uint32_t)er, sig, pad);
+}
+X87_FN bool x80_in_safe_range(const x80 &v) {
+    const int e = v.se & 0x7fff;
+    return (v.m >> 63) && e >= kX80SafeLo && e <= kX80SafeHi;
+}
+
 // C99 Annex G multiply for long double _Complex, as gcc emits it: the inline
 // ac - bd / ad + bc, and __mulxc3's recovery when both parts are NaN.
 X87_FN void x80_cmul(x80 a, x80 b, x80 c, x80 d, x80 &x, x80 &y) {
     const x80 pa = a, pb = b;   // result pads come from the inout element
+    // Fast path: four normal parts of moderate exponent.  The four products
+    // are normal and finite, so x and y can be neither NaN (no recovery) nor
+    // invalid, and x80_addsub's class checks pass straight through.
+    if (__builtin_expect(x80_in_safe_range(a) && x80_in_safe_range(b) && x80_in_safe_range(c) &&
+                         x80_in_safe_range(d), 1)) {
+        x = x80_addsub_normal(x80_mul_safe(a, c, pa), x80_mul_safe(b, d, pa), true, pa);
+        y = x80_addsub_normal(x80_mul_safe(a, d, pb), x80_mul_safe(b, c, pb), false, pb);
+        return;
+    }
     x80 ac = x80_mul(a, c, pa), bd = x80_mul(b, d, pa), ad = x80_mul(a, d, pb), bc = x80_mul(b, c, pb);
     x = x80_sub(ac, bd, pa);
     y = x80_add(ad, bc, pb);

@@ -39,8 +39,8 @@ static x80 gen() {
         e = 0x3fff - 40 + (uint32_t)(rnd() % 80);
         m |= 1ull << 63;
         if (rnd() & 1) m &= ~0ull << (rnd() % 64);   // short significands -> exact / tie cases
-    } else if (k < 52) {     // normal, anywhere
-        e = 1 + (uint32_t)(rnd() % 0x7ffe);
+    } else if (k < 52) {     // normal, anywhere; half of them at the edges of x80_cmul's fast-path range
+        e = (rnd() & 1) ? 1 + (uint32_t)(rnd() % 0x7ffe) : ((rnd() & 1) ? 8200u : 24560u) - 3 + (uint32_t)(rnd() % 7);
         m |= 1ull << 63;
     } else if (k < 60) {     // near the bottom of the range
         e = 1 + (uint32_t)(rnd() % 80);

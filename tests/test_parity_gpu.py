@@ -544,3 +544,38 @@ def test_concurrent_pageable_threads(mpi, orc, cuda):
     assert not errs
     for a, b, want, _ in data:
         assert np.array_equal(a, want)
+
+
+def test_long_double_complex_prod_fast_path_edges(mpi, orc, cuda):
+    """long double _Complex PROD takes a class-check-free path when all four parts
+    are normal with biased exponents in [8200, 24560] (x87.hpp x80_cmul); parts
+    at and just outside those bounds, and products that reach the overflow /
+    underflow edges from inside and outside the range, against the host x87."""
+    rng = np.random.default_rng(0xCB0)
+    n = 4099
+    edges = np.array([8199, 8200, 8201, 16383, 24559, 24560, 24561, 1, 32766, 0], dtype=np.uint16)
+
+    def parts():
+        v = np.zeros(n, dtype=T.X80)
+        e = edges[rng.integers(0, edges.size, n)]
+        m = rng.integers(0, 2 ** 63, n, dtype=np.uint64) | np.uint64(1 << 63)
+        m[e == 0] >>= np.uint64(rng.integers(1, 63))            # denormals
+        v["m"] = m
+        v["se"] = e | (rng.integers(0, 2, n, dtype=np.uint16) << np.uint16(15))
+        v["pad"] = np.frombuffer(rng.bytes(6 * n), dtype="V6")
+        return v
+
+    for _ in range(3):
+        a = np.zeros(n, dtype=T.CX80)
+        b = np.zeros(n, dtype=T.CX80)
+        a["re"], a["im"], b["re"], b["im"] = parts(), parts(), parts(), parts()
+        ab, bb = T.to_bytes(a), T.to_bytes(b)
+        want = ab.copy()
+        t = "MPI_C_LONG_DOUBLE_COMPLEX"
+        assert orc.reduce_local(bb.copy(), want, n, mpi.DATATYPES[t], mpi.OPS["MPI_PROD"]) == 0
+        tio, pio = dev(cuda, ab)
+        tin, pin = dev(cuda, bb)
+        assert mpi.reduce_local(pin, pio, n, mpi.DATATYPES[t], mpi.OPS["MPI_PROD"]) == 0
+        got = back(tio, 0, ab.size)
+        if not same(got, want, t):
+            pytest.fail(explain(got, want, ab, bb, T.elem_size(t)))
