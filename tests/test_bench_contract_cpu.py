@@ -1,0 +1,57 @@
+"""The committed bench line (profiles/r01s4_bench.log, measured on MI355X) against
+the driver's contract and against itself: BASELINE.json's metric, the
+required keys, value = algorithmic bytes x N / time, roofline.frac =
+achieved / peak with achieved = 805,306,368 B / mean launch time, and the
+PMC traffic it quotes equal to profiles/pmc_traffic.json."""
+import json
+import os
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LINE = os.path.join(ROOT, "profiles", "r01s4_bench.log")
+GIB = float(1 << 30)
+
+
+@pytest.fixture(scope="module")
+def line():
+    with open(LINE) as f:
+        rows = [json.loads(ln) for ln in f if ln.startswith("{")]
+    assert rows, "no JSON line in " + LINE
+    return rows[-1]
+
+
+def test_contract_keys(line):
+    with open(os.path.join(ROOT, "BASELINE.json")) as f:
+        base = json.load(f)
+    assert line["metric"] == base["metric"]
+    for k in ("value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+              "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"):
+        assert k in line, k
+    assert line["unit"] == "GiB/s" and line["higher_is_better"] is True and line["scaling"] == "weak"
+    assert line["vs_baseline"] is None          # BASELINE.md publishes no number for this metric
+    assert line["dtype"] == "f32" and "workload" in line["config"]
+    for k in ("bound", "achieved", "peak", "unit", "frac", "traffic"):
+        assert k in line["roofline"], k
+    for k in ("value", "unit", "cores", "kind", "sample"):
+        assert k in line["cpu_baseline"], k
+    assert line["cpu_baseline"]["kind"] in ("port", "reference")
+
+
+def test_value_is_bytes_over_time(line):
+    alg = line["config"]["algorithmic_bytes_per_call"]
+    assert alg == 3 * 256 * (1 << 20)
+    v = alg * line["n_gpus"] / (line["ms_per_step"] * 1e-3) / GIB
+    assert v == pytest.approx(line["value"], rel=2e-3)
+
+
+def test_roofline_is_self_consistent(line):
+    r = line["roofline"]
+    assert r["bound"] == "hbm" and r["unit"] == "GB/s" and r["peak"] == 8000.0
+    assert r["achieved"] == pytest.approx(r["algorithmic_bytes_per_launch"] / (r["mean_launch_us"] * 1e-6) / 1e9,
+                                          rel=2e-3)
+    assert r["frac"] == pytest.approx(r["achieved"] / r["peak"], rel=1e-3)
+    with open(os.path.join(ROOT, "profiles", "pmc_traffic.json")) as f:
+        pmc = json.load(f)
+    assert r["traffic"] == pmc["hbm_bytes_per_launch"]
+    assert 1.0 <= r["traffic"] / r["algorithmic_bytes_per_launch"] < 1.01
