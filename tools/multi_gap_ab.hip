@@ -144,15 +144,14 @@ int main(int argc, char **argv) {
     }
     for (auto &p : outs) CK(hipMalloc(&p, bytes));
     // P = 2 / 4 shapes (the first P operands of a set); algorithmic bytes (P+1) x block
+    // P = 8 (config 4 block at N = 8): longer contiguous runs per operand and wave
     std::vector<Var> vs = {
-        {"TREE2 f32 product (U4 T256)", 4, &launch_combine_p<OpSum, float, 2, true>},
-        {"TREE2 f32 U4 T256 gap2", 4, &launch_mx<float, true, 4, 256, 2, 2>},
-        {"TREE2 f32 U2 T512 gap2", 4, &launch_mx<float, true, 2, 512, 2, 2>},
-        {"TREE2 f32 U1 T1024 gap0", 4, &launch_mx<float, true, 1, 1024, 0, 2>},
-        {"TREE4 f32 product (U2 T256)", 4, &launch_combine_p<OpSum, float, 4, true>},
-        {"TREE4 f32 U2 T512 gap2", 4, &launch_mx<float, true, 2, 512, 2, 4>},
-        {"TREE4 f32 U1 T1024 gap2", 4, &launch_mx<float, true, 1, 1024, 2, 4>},
-        {"TREE4 f32 U4 T256 gap4", 4, &launch_mx<float, true, 4, 256, 4, 4>},
+        {"TREE8 f32 product (U1 T1024)", 4, &launch_combine_p<OpSum, float, 8, true>},
+        {"TREE8 f32 U2 T256 gap4", 4, &launch_mx<float, true, 2, 256, 4>},
+        {"TREE8 f32 U4 T256 gap4", 4, &launch_mx<float, true, 4, 256, 4>},
+        {"TREE8 f32 U4 T256 gap0", 4, &launch_mx<float, true, 4, 256, 0>},
+        {"TREE8 f32 U4 T128 gap4", 4, &launch_mx<float, true, 4, 128, 4>},
+        {"TREE8 f32 U2 T1024 gap4", 4, &launch_mx<float, true, 2, 1024, 4>},
     };
     hipStream_t st;
     CK(hipStreamCreate(&st));
