@@ -14,8 +14,9 @@
 //     by ILP + 8 waves/CU of TLP), with a one-instruction issue gap after
 //     each (inout, in) pair (issue_gap below: 0.810 -> 0.830-0.841 of peak);
 //   * buffer_load/store_dwordx4 with the `nt` cache policy (aux = 2) on both
-//     operands and on the store: streamed-once data should not displace L2 /
-//     Infinity Cache lines; measured 0.81 of the 8 TB/s HBM peak vs 0.70 for
+//     operands and on the store (sc1 on the store for results <= 64 MiB, which
+//     then stay in the Infinity Cache for their next reader: kKeepBytes below):
+//     streamed-once data should not displace L2 / Infinity Cache lines; measured 0.81 of the 8 TB/s HBM peak vs 0.70 for
 //     default-policy loads and 0.63 for a grid-stride loop (before the gap);
 //   * the buffer descriptor covers exactly this tile's bytes, so the ragged
 //     last tile needs no branch: out-of-range loads return 0 and out-of-range
@@ -34,8 +35,25 @@ constexpr int kThreads = 256;
 constexpr int kVecPerLane = 4;
 constexpr uint32_t kTileBytes = kThreads * kVecPerLane * 16;  // 16 KiB per operand
 constexpr int kCachePolicyNT = 2;                             // aux bit: nt
+constexpr int kCachePolicySC1 = 16;                           // aux bit: sc1 (device scope)
+// Results of at most kKeepBytes are stored with sc1 instead of nt: such a
+// store allocates in the 256 MB Infinity Cache (MALL), where the next schedule
+// step (or the RCCL send of the block) finds it; nt stores bypass it.  Over
+// operands nothing re-reads both store the same (64 MiB with 16 rotating
+// pairs: 33.9 vs 33.4 us; 32 MiB: 19.0 vs 18.8 us); with the output read
+// again within ~256 MiB of traffic sc1 wins (64 MiB, 4 pairs: 27.0 vs
+// 33.2 us); at 256 MiB it is 2 % slower, so large results keep nt
+// (tools/sync_store_ab.hip, profiles/r01s4_sync_store_ab.log).
+constexpr uint64_t kKeepBytes = 64ull << 20;
+
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+// one 16-byte store; `keep` (uniform: derived from the launch size) picks sc1
+__device__ __forceinline__ void store16(u32x4 v, __amdgpu_buffer_rsrc_t r, int off, bool keep) {
+    if (keep) __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, kCachePolicySC1);
+    else __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, kCachePolicyNT);
+}
 
 template <class T>
 struct Pack16 {
@@ -112,9 +130,9 @@ __device__ __forceinline__ void reduce_tile(const char *in, char *io, uint64_t b
         b[u] = __builtin_amdgcn_raw_buffer_load_b128(rin, wb + u * 1024, 0, kCachePolicyNT);
         if (u + 1 < kVecPerLane) issue_gap();
     }
+    const bool keep = vbytes <= kKeepBytes;
 #pragma unroll
-    for (int u = 0; u < kVecPerLane; ++u)
-        __builtin_amdgcn_raw_buffer_store_b128(combine16<Op, T>(a[u], b[u]), rio, wb + u * 1024, 0, kCachePolicyNT);
+    for (int u = 0; u < kVecPerLane; ++u) store16(combine16<Op, T>(a[u], b[u]), rio, wb + u * 1024, keep);
 }
 
 // With head / tail elements (nhead or ntail != 0), workgroup 0 combines them
@@ -225,8 +243,7 @@ __global__ __launch_bounds__(kThreads) void k_reduce_shift(ShiftArgs<T> args) {
             nb.y = (__shfl_down(b[u].y, 1, 64) & keep) | n63[u].y;
             nb.z = (__shfl_down(b[u].z, 1, 64) & keep) | n63[u].z;
             nb.w = (__shfl_down(b[u].w, 1, 64) & keep) | n63[u].w;
-            __builtin_amdgcn_raw_buffer_store_b128(combine16<Op, T>(a[u], funnel16(b[u], nb, args.delta)), rio, off,
-                                                   0, kCachePolicyNT);
+            store16(combine16<Op, T>(a[u], funnel16(b[u], nb, args.delta)), rio, off, ta.vbytes <= kKeepBytes);
         }
     }
     if (blockIdx.x == 0) {
@@ -384,7 +401,7 @@ __global__ __launch_bounds__(kThreads) void k_reduce_tile_wide(const char *in, c
     __syncthreads();
 #pragma unroll
     for (int v = 0; v < NV; ++v)
-        __builtin_amdgcn_raw_buffer_store_b128(sa[wv + v * 64], rio, (wv + v * 64) * 16, 0, kCachePolicyNT);
+        store16(sa[wv + v * 64], rio, (wv + v * 64) * 16, nbytes <= kKeepBytes);
 }
 
 // EPL: elements per lane (2 for the memory-bound ops; the compute-bound soft
@@ -511,7 +528,7 @@ __global__ __launch_bounds__(TH) void k_combine_multi(MultiArgs a) {
                 for (int j = 0; j < P; ++j) v[j] = pk[j].e[k];
                 res.e[k] = fold_fast<Op, T, P, TREE>(v);
             }
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, res), ro, wb + u * 1024, 0, kCachePolicyNT);
+            store16(__builtin_bit_cast(u32x4, res), ro, wb + u * 1024, a.vbytes <= kKeepBytes);
         }
     }
     if (blockIdx.x == 0) {
