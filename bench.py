@@ -50,7 +50,9 @@ NPAIRS = 4                     # operand pairs rotated through (>= 3, SURVEY.md 
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="ranks (one per GPU); without WORLD_SIZE in the environment, N > 1 starts N ranks "
+                         "itself through torch.distributed.run before any GPU call")
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--mib", type=int, default=256, help="MiB per operand (metric: 256)")
@@ -60,7 +62,64 @@ def parse():
     ap.add_argument("--cpu-iters", type=int, default=48)
     ap.add_argument("--collectives", choices=["auto", "on", "off"], default="auto",
                     help="configs 4-5 via bench_coll.py in isolated child processes (auto: when N > 1)")
+    ap.add_argument("--cpu-standin", action="store_true",
+                    help="TEST ONLY: gloo + a numpy step instead of the GPU call, to exercise the rank "
+                         "launch and the max-over-ranks timing on a machine without GPUs")
     return ap.parse_args()
+
+
+def spawn_ranks(args) -> int | None:
+    """`python bench.py --gpus N` with no WORLD_SIZE: start N ranks (one per GPU)
+    through torch.distributed.run on 127.0.0.1 and return their exit code.
+    Called before anything touches a GPU; the ranks find WORLD_SIZE set and
+    run main() themselves, rank 0 printing the JSON line."""
+    if args.gpus <= 1 or "WORLD_SIZE" in os.environ:
+        return None
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
+def cpu_standin(args) -> None:
+    """TEST ONLY (--cpu-standin): the rank plumbing of main() with gloo and a
+    numpy a += b step, so a CPU test can check that `bench.py --gpus N` runs N
+    ranks and reports n_gpus = N.  Never a measurement."""
+    import numpy as np
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if world > 1:
+        dist.init_process_group(backend="gloo")
+    import torch
+    a = np.ones(1 << 16, np.float32)
+    b = np.ones(1 << 16, np.float32)
+
+    def step(i):
+        np.add(a, b, out=a)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    def max_over_ranks(x):
+        if world == 1:
+            return x
+        t = torch.tensor([x], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    dt = time_steps(step, args.steps, args.warmup, lambda: None, barrier, max_over_ranks)
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": None, "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
+                          "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 4),
+                          "data": "cpu stand-in (test only, not a measurement)"}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
 
 
 def time_steps(step, k: int, w: int, sync, barrier, max_over_ranks) -> float:
@@ -215,6 +274,11 @@ def host_cpu(affinity: int) -> str:
 
 def main():
     args = parse()
+    rc = spawn_ranks(args)
+    if rc is not None:
+        sys.exit(rc)
+    if args.cpu_standin:
+        return cpu_standin(args)
     import torch
     import torch.distributed as dist
     import mpich_pip_amd as m
@@ -223,7 +287,8 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE", file=sys.stderr)
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world} (launched by an external launcher); "
+              f"measuring WORLD_SIZE ranks", file=sys.stderr)
     torch.cuda.set_device(local)
     if world > 1:
         dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))

@@ -30,6 +30,19 @@ namespace {
 namespace mpir_hip {
 Entry g_table[MPIR_HIP_NOPS][MPIR_HIP_NELEMS];
 multi_fn g_multi[MPIR_HIP_NOPS][MPIR_HIP_NELEMS][2][3];
+
+// Bytes at the end of each result stored sc1 (into the Infinity Cache) rather
+// than nt: MPIR_CVAR_REDUCE_LOCAL_KEEP_MB (0 = every store nt), default 64
+// (reduce_kernels.hpp, kKeepBytes).
+uint64_t keep_bytes() {
+    static const uint64_t v = [] {
+        const char *e = getenv("MPIR_CVAR_REDUCE_LOCAL_KEEP_MB");
+        if (!e) return kKeepBytes;
+        const long mb = atol(e);
+        return (uint64_t)(mb >= 0 && mb <= 4096 ? mb : 64) << 20;
+    }();
+    return v;
+}
 }  // namespace mpir_hip
 
 namespace {

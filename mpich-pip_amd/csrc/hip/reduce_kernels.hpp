@@ -14,8 +14,8 @@
 //     by ILP + 8 waves/CU of TLP), with a one-instruction issue gap after
 //     each (inout, in) pair (issue_gap below: 0.810 -> 0.830-0.841 of peak);
 //   * buffer_load/store_dwordx4 with the `nt` cache policy (aux = 2) on both
-//     operands and on the store (sc1 on the store for results <= 64 MiB, which
-//     then stay in the Infinity Cache for their next reader: kKeepBytes below):
+//     operands and on the store (sc1 on the stores of the last 64 MiB of a
+//     result, which stay in the Infinity Cache: kKeepBytes below):
 //     streamed-once data should not displace L2 / Infinity Cache lines; measured 0.81 of the 8 TB/s HBM peak vs 0.70 for
 //     default-policy loads and 0.63 for a grid-stride loop (before the gap);
 //   * the buffer descriptor covers exactly this tile's bytes, so the ragged
@@ -36,20 +36,34 @@ constexpr int kVecPerLane = 4;
 constexpr uint32_t kTileBytes = kThreads * kVecPerLane * 16;  // 16 KiB per operand
 constexpr int kCachePolicyNT = 2;                             // aux bit: nt
 constexpr int kCachePolicySC1 = 16;                           // aux bit: sc1 (device scope)
-// Results of at most kKeepBytes are stored with sc1 instead of nt: such a
-// store allocates in the 256 MB Infinity Cache (MALL), where the next schedule
-// step (or the RCCL send of the block) finds it; nt stores bypass it.  Over
-// operands nothing re-reads both store the same (64 MiB with 16 rotating
-// pairs: 33.9 vs 33.4 us; 32 MiB: 19.0 vs 18.8 us); with the output read
-// again within ~256 MiB of traffic sc1 wins (64 MiB, 4 pairs: 27.0 vs
-// 33.2 us); at 256 MiB it is 2 % slower, so large results keep nt
-// (tools/sync_store_ab.hip, profiles/r01s4_sync_store_ab.log).
+// The LAST `keep` bytes of every result (default kKeepBytes = 64 MiB; the
+// launchers pass keep_bytes(), i.e. MPIR_CVAR_REDUCE_LOCAL_KEEP_MB) are stored
+// with sc1 instead of nt.  An sc1 store allocates in the 256 MB Infinity Cache
+// (MALL), an nt store bypasses it.  Two effects, both measured on MI355X:
+//   * a result of at most 64 MiB stays in the MALL for its next reader (the
+//     next schedule step, the RCCL send of a block, the D2H copy of a staged
+//     chunk): 64 MiB re-read within ~256 MiB of traffic 27.0 vs 33.2 us
+//     (tools/sync_store_ab.hip, profiles/r01s4_sync_store_ab.log);
+//   * for a larger result, the write-back of its last 64 MiB drains from the
+//     MALL after the launch instead of inside it, so a synchronous call's
+//     kernel body ends earlier: 256 MiB fp32 SUM body 118.4-118.9 us vs
+//     120.6-121.1 (all nt), call 126.8-127.6 vs 128.8-129.4 us; the last
+//     96 MiB or more stored sc1 is slower than none (the MALL thrashes), and
+//     so is any mix spread over the whole launch (tools/aql/aql2.cpp,
+//     profiles/r02/store_tail_sweep.log).
+// Nothing else changes: the bytes reach HBM either way (MALL is memory-side).
 constexpr uint64_t kKeepBytes = 64ull << 20;
+uint64_t keep_bytes();   // MPIR_CVAR_REDUCE_LOCAL_KEEP_MB, default kKeepBytes (hip_reduce.hip)
+
+// true for a tile that starts inside the last `keep` bytes of a `vbytes` region
+__device__ __forceinline__ bool keep_tile(uint64_t base, uint64_t vbytes, uint64_t keep) {
+    return vbytes - base <= keep;
+}
 
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
-// one 16-byte store; `keep` (uniform: derived from the launch size) picks sc1
+// one 16-byte store; `keep` (uniform per workgroup: keep_tile) picks sc1
 __device__ __forceinline__ void store16(u32x4 v, __amdgpu_buffer_rsrc_t r, int off, bool keep) {
     if (keep) __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, kCachePolicySC1);
     else __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, kCachePolicyNT);
@@ -72,6 +86,7 @@ struct TileArgs {
     const T *tail_in;   // elements after the vector region
     T *tail_io;
     uint32_t ntail;
+    uint64_t keep;      // keep_bytes(): the last `keep` bytes are stored sc1
 };
 
 template <class Op, class T>
@@ -116,7 +131,7 @@ __device__ __forceinline__ void issue_gap() {
 // One 16 KiB tile per operand: each wave owns a contiguous 4 KiB of it (one
 // 1 KiB lane-contiguous access per instruction).
 template <class Op, class T>
-__device__ __forceinline__ void reduce_tile(const char *in, char *io, uint64_t base, uint64_t vbytes) {
+__device__ __forceinline__ void reduce_tile(const char *in, char *io, uint64_t base, uint64_t vbytes, uint64_t keepb) {
     const uint64_t left = vbytes - base;
     const int nrec = (int)(left < kTileBytes ? left : kTileBytes);
     __amdgpu_buffer_rsrc_t rin = __builtin_amdgcn_make_buffer_rsrc((void *)(in + base), 0, nrec, 0x00020000);
@@ -130,7 +145,7 @@ __device__ __forceinline__ void reduce_tile(const char *in, char *io, uint64_t b
         b[u] = __builtin_amdgcn_raw_buffer_load_b128(rin, wb + u * 1024, 0, kCachePolicyNT);
         if (u + 1 < kVecPerLane) issue_gap();
     }
-    const bool keep = vbytes <= kKeepBytes;
+    const bool keep = keep_tile(base, vbytes, keepb);
 #pragma unroll
     for (int u = 0; u < kVecPerLane; ++u) store16(combine16<Op, T>(a[u], b[u]), rio, wb + u * 1024, keep);
 }
@@ -140,7 +155,7 @@ __device__ __forceinline__ void reduce_tile(const char *in, char *io, uint64_t b
 template <class Op, class T>
 __device__ __forceinline__ void reduce_tile_body(const TileArgs<T> &args) {
     const uint64_t base = (uint64_t)blockIdx.x * kTileBytes;
-    if (base < args.vbytes) reduce_tile<Op, T>(args.in, args.io, base, args.vbytes);
+    if (base < args.vbytes) reduce_tile<Op, T>(args.in, args.io, base, args.vbytes, args.keep);
     if (blockIdx.x == 0) {
         Op op;
         const unsigned t = threadIdx.x;
@@ -155,12 +170,12 @@ __global__ __launch_bounds__(kThreads) void k_reduce_tile(TileArgs<T> args) {
 }
 
 // No head / tail (the common case: 16 B-aligned buffers, bytes a multiple of
-// 16): three scalar arguments and nothing after the tile.
+// 16): four scalar arguments and nothing after the tile.
 template <class Op, class T>
-__global__ __launch_bounds__(kThreads) void k_reduce_tile_lean(const char *in, char *io, uint64_t vbytes) {
+__global__ __launch_bounds__(kThreads) void k_reduce_tile_lean(const char *in, char *io, uint64_t vbytes, uint64_t keep) {
     const uint64_t base = (uint64_t)blockIdx.x * kTileBytes;
     if (base >= vbytes) return;
-    reduce_tile<Op, T>(in, io, base, vbytes);
+    reduce_tile<Op, T>(in, io, base, vbytes, keep);
 }
 
 // inbuf misaligned relative to inoutbuf: (in - io) mod 16 = delta != 0, the
@@ -243,7 +258,7 @@ __global__ __launch_bounds__(kThreads) void k_reduce_shift(ShiftArgs<T> args) {
             nb.y = (__shfl_down(b[u].y, 1, 64) & keep) | n63[u].y;
             nb.z = (__shfl_down(b[u].z, 1, 64) & keep) | n63[u].z;
             nb.w = (__shfl_down(b[u].w, 1, 64) & keep) | n63[u].w;
-            store16(combine16<Op, T>(a[u], funnel16(b[u], nb, args.delta)), rio, off, ta.vbytes <= kKeepBytes);
+            store16(combine16<Op, T>(a[u], funnel16(b[u], nb, args.delta)), rio, off, keep_tile(base, ta.vbytes, ta.keep));
         }
     }
     if (blockIdx.x == 0) {
@@ -308,13 +323,14 @@ hipError_t launch_reduce(const void *in_, void *io_, uint64_t count, hipStream_t
         a.tail_in = reinterpret_cast<const T *>(in + head_bytes + vbytes);
         a.tail_io = reinterpret_cast<T *>(io + head_bytes + vbytes);
         a.ntail = (uint32_t)((rest - vbytes) / sizeof(T));
+        a.keep = keep_bytes();
         uint64_t grid = (vbytes + kTileBytes - 1) / kTileBytes;
         if (grid == 0) grid = 1;
         if (a.nhead || a.ntail)
             hipLaunchKernelGGL((k_reduce_tile<Op, T>), dim3((unsigned)grid), dim3(kThreads), 0, s, a);
         else
             hipLaunchKernelGGL((k_reduce_tile_lean<Op, T>), dim3((unsigned)grid), dim3(kThreads), 0, s, a.in, a.io,
-                               a.vbytes);
+                               a.vbytes, a.keep);
     } else if ((ao % alignof(T) == 0) && head0 % sizeof(T) == 0 && nbytes >= 2 * kTileBytes) {
         // inoutbuf element-aligned, inbuf at any other offset mod 16: the
         // aligned-load + shuffle + funnel tile kernel (small counts stay
@@ -332,6 +348,7 @@ hipError_t launch_reduce(const void *in_, void *io_, uint64_t count, hipStream_t
         a.t.tail_in = reinterpret_cast<const T *>(in + head_bytes + vbytes);
         a.t.tail_io = reinterpret_cast<T *>(io + head_bytes + vbytes);
         a.t.ntail = (uint32_t)((rest - vbytes) / sizeof(T));
+        a.t.keep = keep_bytes();
         const uintptr_t vin = ai + head_bytes;
         a.delta = (uint32_t)(vin & 15);
         a.in_al = reinterpret_cast<const char *>(vin - a.delta);
@@ -359,7 +376,7 @@ hipError_t launch_reduce(const void *in_, void *io_, uint64_t count, hipStream_t
 // 128-byte line fetched twice under `nt`).  The buffer range check handles
 // the ragged last tile (zeros in, stores dropped).
 template <class Op, class T, int EPL>
-__global__ __launch_bounds__(kThreads) void k_reduce_tile_wide(const char *in, char *io, uint64_t nbytes) {
+__global__ __launch_bounds__(kThreads) void k_reduce_tile_wide(const char *in, char *io, uint64_t nbytes, uint64_t keep) {
     static_assert(sizeof(T) == 32, "two 16-byte halves per element");
     constexpr int NV = 2 * EPL;                       // 16-byte vectors per lane per operand
     constexpr uint32_t tile = kThreads * NV * 16;
@@ -401,7 +418,7 @@ __global__ __launch_bounds__(kThreads) void k_reduce_tile_wide(const char *in, c
     __syncthreads();
 #pragma unroll
     for (int v = 0; v < NV; ++v)
-        store16(sa[wv + v * 64], rio, (wv + v * 64) * 16, nbytes <= kKeepBytes);
+        store16(sa[wv + v * 64], rio, (wv + v * 64) * 16, keep_tile(base, nbytes, keep));
 }
 
 // EPL: elements per lane (2 for the memory-bound ops; the compute-bound soft
@@ -418,7 +435,8 @@ hipError_t launch_reduce_wide(const void *in_, void *io_, uint64_t count, hipStr
         const uint64_t nbytes = count * sizeof(T);
         uint64_t grid = (nbytes + tile - 1) / tile;
         if (grid == 0) grid = 1;
-        hipLaunchKernelGGL((k_reduce_tile_wide<Op, T, EPL>), dim3((unsigned)grid), dim3(kThreads), 0, s, in, io, nbytes);
+        hipLaunchKernelGGL((k_reduce_tile_wide<Op, T, EPL>), dim3((unsigned)grid), dim3(kThreads), 0, s, in, io, nbytes,
+                           keep_bytes());
         return hipGetLastError();
     }
     uint64_t grid = (count + kThreads - 1) / kThreads;
@@ -453,6 +471,7 @@ struct MultiArgs {
     uint64_t vbytes;                // multiple of 16
     uint32_t nhead, ntail;          // scalar elements before / after the vector region
     int64_t head_off, tail_off;     // byte offsets of head / tail from the region starts
+    uint64_t keep;                  // keep_bytes()
 };
 
 template <class Op, class T, int P, bool TREE, bool RAW = false>
@@ -528,7 +547,7 @@ __global__ __launch_bounds__(TH) void k_combine_multi(MultiArgs a) {
                 for (int j = 0; j < P; ++j) v[j] = pk[j].e[k];
                 res.e[k] = fold_fast<Op, T, P, TREE>(v);
             }
-            store16(__builtin_bit_cast(u32x4, res), ro, wb + u * 1024, a.vbytes <= kKeepBytes);
+            store16(__builtin_bit_cast(u32x4, res), ro, wb + u * 1024, keep_tile(base, a.vbytes, a.keep));
         }
     }
     if (blockIdx.x == 0) {
@@ -573,6 +592,7 @@ hipError_t launch_combine_pu(const void *const *ins, void *out_, uint64_t count,
     }
     MultiArgs a;
     for (int j = 0; j < kMaxOperands; ++j) a.in[j] = j < P ? static_cast<const char *>(ins[j]) : nullptr;
+    a.keep = keep_bytes();
     if (vec_ok) {
         uint64_t head = (16 - (ao & 15)) & 15;
         if (head > nbytes) head = nbytes;

@@ -1,0 +1,231 @@
+// sync_split.hip -- where the time of a synchronous 256 MiB MPI_Reduce_local
+// goes, and whether a kernel that signals its own completion beats the
+// product's launch + hipStreamWriteValue32 (a second, blit dispatch) + spin.
+//
+// Variants, each a loop of K synchronous calls over 4 rotating 256 MiB fp32
+// pairs (the bench protocol), per-call wall time (mean and median):
+//   flag      tile kernel (nt stores) + hipStreamWriteValue32 + host spin   [product]
+//   sync      tile kernel (nt stores) + hipStreamSynchronize
+//   self_sc1  tile kernel with sc1 stores; every workgroup, after all its waves'
+//             stores are acknowledged (s_waitcnt vmcnt(0) + barrier), adds to one of
+//             S sharded device counters; the workgroup completing a shard adds to
+//             the top counter; the one completing the top writes the host word.
+//             No second dispatch; the host spins on the word.
+//   self_nt   the same with nt stores (NOT a valid hand-off: nt lines can stay
+//             dirty in the XCD L2 -- timing reference only)
+// plus kernel-only durations (HIP events, median) of the three kernel flavours and
+// the host cost of hipPointerGetAttributes and of one hipLaunchKernel.
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -o tools/sync_split tools/sync_split.hip
+#include <hip/hip_runtime.h>
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP %s line %d\n", hipGetErrorString(e_), __LINE__); exit(2);} } while (0)
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+constexpr int kThreads = 256;
+constexpr uint32_t kTile = 16384;
+
+__device__ __forceinline__ void gap() {
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_nop 0");
+    __builtin_amdgcn_sched_barrier(0);
+}
+
+// STORE: 2 = nt, 16 = sc1.  SELF: the sharded completion counter.
+template <int STORE, bool SELF>
+__global__ __launch_bounds__(kThreads) void k_tile(const char *in, char *io, uint64_t vbytes, uint32_t *cnt,
+                                                   uint32_t nsh, uint32_t *hflag, uint32_t seq) {
+    const uint64_t base = (uint64_t)blockIdx.x * kTile;
+    if (base < vbytes) {
+        const uint64_t left = vbytes - base;
+        const int nrec = (int)(left < kTile ? left : kTile);
+        __amdgpu_buffer_rsrc_t rin = __builtin_amdgcn_make_buffer_rsrc((void *)(in + base), 0, nrec, 0x00020000);
+        __amdgpu_buffer_rsrc_t rio = __builtin_amdgcn_make_buffer_rsrc((void *)(io + base), 0, nrec, 0x00020000);
+        const int t = (int)threadIdx.x;
+        const int wb = (t >> 6) * 4096 + (t & 63) * 16;
+        u32x4 a[4], b[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            a[u] = __builtin_amdgcn_raw_buffer_load_b128(rio, wb + u * 1024, 0, 2);
+            b[u] = __builtin_amdgcn_raw_buffer_load_b128(rin, wb + u * 1024, 0, 2);
+            if (u < 3) gap();
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            f32x4 r = __builtin_bit_cast(f32x4, a[u]) + __builtin_bit_cast(f32x4, b[u]);
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, r), rio, wb + u * 1024, 0, STORE);
+        }
+    }
+    if constexpr (SELF) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            const uint32_t sh = blockIdx.x % nsh;
+            const uint32_t expect = gridDim.x / nsh + (sh < gridDim.x % nsh ? 1u : 0u);
+            const uint32_t old = __hip_atomic_fetch_add(cnt + sh * 32, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (old + 1 == expect) {
+                __hip_atomic_store(cnt + sh * 32, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const uint32_t top = __hip_atomic_fetch_add(cnt + nsh * 32, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (top + 1 == nsh) {
+                    __hip_atomic_store(cnt + nsh * 32, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_store(hflag, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                }
+            }
+        }
+    }
+}
+
+static double now() { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); }
+
+int main(int argc, char **argv) {
+    const int K = argc > 1 ? atoi(argv[1]) : 100;
+    const int rounds = argc > 2 ? atoi(argv[2]) : 4;
+    hipStream_t s;
+    CK(hipStreamCreate(&s));
+    volatile uint32_t *flag;
+    CK(hipHostMalloc((void **)&flag, 64, hipHostMallocCoherent | hipHostMallocMapped));
+    *flag = 0;
+    uint32_t seq = 0;
+    uint32_t *cnt;
+    CK(hipMalloc(&cnt, 4096 * 4));
+    CK(hipMemset(cnt, 0, 4096 * 4));
+    const uint64_t bytes = 256ull << 20;
+    const uint64_t n = bytes / 4;
+    std::vector<float *> bufs(8);
+    std::vector<float> h(n);
+    srand(1);
+    for (auto &x : h) x = (float)rand() / RAND_MAX * 2 - 1;
+    for (auto &b : bufs) { CK(hipMalloc(&b, bytes)); CK(hipMemcpy(b, h.data(), bytes, hipMemcpyHostToDevice)); }
+    CK(hipDeviceSynchronize());
+    const unsigned grid = (unsigned)(bytes / kTile);
+    auto in = [&](int i) { return (const char *)bufs[2 * (i & 3)]; };
+    auto io = [&](int i) { return (char *)bufs[2 * (i & 3) + 1]; };
+    const double alg = 3.0 * bytes;
+
+    // ---- host costs
+    {
+        hipPointerAttribute_t at;
+        const int N = 20000;
+        double t0 = now();
+        for (int i = 0; i < N; ++i) CK(hipPointerGetAttributes(&at, in(i)));
+        double t1 = now();
+        printf("host hipPointerGetAttributes: %.3f us/call (device ptr)\n", (t1 - t0) / N * 1e6);
+        std::vector<float> hostv(16);
+        t0 = now();
+        for (int i = 0; i < N; ++i) { (void)hipPointerGetAttributes(&at, hostv.data()); (void)hipGetLastError(); }
+        t1 = now();
+        printf("host hipPointerGetAttributes: %.3f us/call (pageable host ptr)\n", (t1 - t0) / N * 1e6);
+        // launch cost of the real kernel (queue fills; host time only)
+        CK(hipDeviceSynchronize());
+        t0 = now();
+        for (int i = 0; i < 40; ++i)
+            hipLaunchKernelGGL((k_tile<2, false>), dim3(grid), dim3(kThreads), 0, s, in(i), io(i), bytes, cnt, 1u, (uint32_t *)flag, 0u);
+        t1 = now();
+        CK(hipStreamSynchronize(s));
+        printf("host hipLaunchKernel: %.3f us/launch (40 queued)\n", (t1 - t0) / 40 * 1e6);
+    }
+
+    const int nsh_list[] = {8, 64, 256};
+    for (int r = 0; r < rounds; ++r) {
+        // ---- kernel-only durations (events)
+        hipEvent_t e0, e1;
+        CK(hipEventCreate(&e0));
+        CK(hipEventCreate(&e1));
+        auto kern_us = [&](auto launch) {
+            std::vector<float> ms;
+            for (int i = 0; i < 5; ++i) launch(i);
+            for (int i = 0; i < 31; ++i) {
+                CK(hipEventRecord(e0, s));
+                launch(i);
+                CK(hipEventRecord(e1, s));
+                CK(hipEventSynchronize(e1));
+                float x;
+                CK(hipEventElapsedTime(&x, e0, e1));
+                ms.push_back(x);
+            }
+            std::sort(ms.begin(), ms.end());
+            return ms[ms.size() / 2] * 1e3;
+        };
+        double k_nt = kern_us([&](int i) {
+            hipLaunchKernelGGL((k_tile<2, false>), dim3(grid), dim3(kThreads), 0, s, in(i), io(i), bytes, cnt, 1u, (uint32_t *)flag, 0u);
+        });
+        double k_sc1 = kern_us([&](int i) {
+            hipLaunchKernelGGL((k_tile<16, false>), dim3(grid), dim3(kThreads), 0, s, in(i), io(i), bytes, cnt, 1u, (uint32_t *)flag, 0u);
+        });
+        double k_self = kern_us([&](int i) {
+            hipLaunchKernelGGL((k_tile<16, true>), dim3(grid), dim3(kThreads), 0, s, in(i), io(i), bytes, cnt, 64u, (uint32_t *)flag, ++seq);
+        });
+        CK(hipStreamSynchronize(s));
+        printf("round %d kernel-only median: nt %.2f us (%.4f) | sc1 %.2f us (%.4f) | sc1+counter(64) %.2f us (%.4f)\n", r,
+               k_nt, alg / (k_nt * 1e-6) / 8e12, k_sc1, alg / (k_sc1 * 1e-6) / 8e12, k_self, alg / (k_self * 1e-6) / 8e12);
+
+        // ---- synchronous loops
+        auto loop = [&](const char *name, auto call) {
+            std::vector<double> per(K);
+            for (int i = 0; i < 5; ++i) call(i);
+            const double T0 = now();
+            for (int i = 0; i < K; ++i) {
+                const double a = now();
+                call(i);
+                per[i] = now() - a;
+            }
+            const double T1 = now();
+            std::sort(per.begin(), per.end());
+            const double mean = (T1 - T0) / K;
+            printf("round %d %-12s mean %8.2f us (%6.1f GiB/s = %.4f) median %8.2f p10 %8.2f p90 %8.2f\n", r, name,
+                   mean * 1e6, alg / mean / (1u << 30), alg / mean / 8e12, per[K / 2] * 1e6, per[K / 10] * 1e6,
+                   per[K * 9 / 10] * 1e6);
+        };
+        loop("flag", [&](int i) {
+            hipLaunchKernelGGL((k_tile<2, false>), dim3(grid), dim3(kThreads), 0, s, in(i), io(i), bytes, cnt, 1u, (uint32_t *)flag, 0u);
+            CK(hipStreamWriteValue32(s, (void *)flag, ++seq, 0));
+            while (*flag != seq) __builtin_ia32_pause();
+        });
+        loop("sync", [&](int i) {
+            hipLaunchKernelGGL((k_tile<2, false>), dim3(grid), dim3(kThreads), 0, s, in(i), io(i), bytes, cnt, 1u, (uint32_t *)flag, 0u);
+            CK(hipStreamSynchronize(s));
+        });
+        for (uint32_t nsh : nsh_list) {
+            char name[32];
+            snprintf(name, sizeof name, "self_sc1/%u", nsh);
+            loop(name, [&](int i) {
+                const uint32_t q = ++seq;
+                hipLaunchKernelGGL((k_tile<16, true>), dim3(grid), dim3(kThreads), 0, s, in(i), io(i), bytes, cnt, nsh, (uint32_t *)flag, q);
+                while (*flag != q) __builtin_ia32_pause();
+            });
+        }
+        loop("self_nt/64", [&](int i) {
+            const uint32_t q = ++seq;
+            hipLaunchKernelGGL((k_tile<2, true>), dim3(grid), dim3(kThreads), 0, s, in(i), io(i), bytes, cnt, 64u, (uint32_t *)flag, q);
+            while (*flag != q) __builtin_ia32_pause();
+        });
+        CK(hipStreamSynchronize(s));
+        CK(hipGetLastError());
+    }
+    // correctness spot check of the self-completing kernel: after the flag the
+    // result must already be in memory (read back with a D2H copy on another
+    // stream, which HIP does not order after the kernel)
+    {
+        hipStream_t s2;
+        CK(hipStreamCreateWithFlags(&s2, hipStreamNonBlocking));
+        std::vector<float> a(n), b(n), got(n);
+        CK(hipMemcpy(a.data(), io(0), bytes, hipMemcpyDeviceToHost));
+        CK(hipMemcpy(b.data(), in(0), bytes, hipMemcpyDeviceToHost));
+        const uint32_t q = ++seq;
+        hipLaunchKernelGGL((k_tile<16, true>), dim3(grid), dim3(kThreads), 0, s, in(0), io(0), bytes, cnt, 64u, (uint32_t *)flag, q);
+        while (*flag != q) __builtin_ia32_pause();
+        CK(hipMemcpyAsync(got.data(), io(0), bytes, hipMemcpyDeviceToHost, s2));
+        CK(hipStreamSynchronize(s2));
+        size_t bad = 0;
+        for (uint64_t i = 0; i < n; ++i) bad += (got[i] != a[i] + b[i]);
+        printf("self_sc1 readback on another stream right after the flag: %zu mismatches of %llu\n", bad, (unsigned long long)n);
+        CK(hipStreamSynchronize(s));
+    }
+    return 0;
+}
