@@ -41,19 +41,19 @@ typedef int MPI_Comm;
 #define MPI_ERR_COMM  5
 #define MPI_ERR_ROOT  7
 
-int MPI_Init(int *argc, char ***argv);
-int MPI_Initialized(int *flag);
-int MPI_Finalize(void);
-int MPI_Finalized(int *flag);
-int MPI_Abort(MPI_Comm comm, int errorcode);
-int MPI_Comm_size(MPI_Comm comm, int *size);
-int MPI_Comm_rank(MPI_Comm comm, int *rank);
-int MPI_Get_processor_name(char *name, int *resultlen);
-double MPI_Wtime(void);
-double MPI_Wtick(void);
-int MPI_Barrier(MPI_Comm comm);
-int MPI_Bcast(void *buffer, int count, MPI_Datatype datatype, int root, MPI_Comm comm);
-int MPI_Reduce(const void *sendbuf, void *recvbuf, int count, MPI_Datatype datatype, MPI_Op op, int root,
+MPICH_API_PUBLIC int MPI_Init(int *argc, char ***argv);
+MPICH_API_PUBLIC int MPI_Initialized(int *flag);
+MPICH_API_PUBLIC int MPI_Finalize(void);
+MPICH_API_PUBLIC int MPI_Finalized(int *flag);
+MPICH_API_PUBLIC int MPI_Abort(MPI_Comm comm, int errorcode);
+MPICH_API_PUBLIC int MPI_Comm_size(MPI_Comm comm, int *size);
+MPICH_API_PUBLIC int MPI_Comm_rank(MPI_Comm comm, int *rank);
+MPICH_API_PUBLIC int MPI_Get_processor_name(char *name, int *resultlen);
+MPICH_API_PUBLIC double MPI_Wtime(void);
+MPICH_API_PUBLIC double MPI_Wtick(void);
+MPICH_API_PUBLIC int MPI_Barrier(MPI_Comm comm);
+MPICH_API_PUBLIC int MPI_Bcast(void *buffer, int count, MPI_Datatype datatype, int root, MPI_Comm comm);
+MPICH_API_PUBLIC int MPI_Reduce(const void *sendbuf, void *recvbuf, int count, MPI_Datatype datatype, MPI_Op op, int root,
                MPI_Comm comm);
 
 #ifdef __cplusplus

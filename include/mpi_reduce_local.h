@@ -42,6 +42,18 @@
 extern "C" {
 #endif
 
+/* The public API stays exported when these sources are compiled into a
+ * libmpi built with -fvisibility=hidden (MPICH's configure.ac:1443 adds it;
+ * mpi.h.in:13 marks the public prototypes the same way); the MPIR_ internals
+ * follow the build's visibility, as MPICH's do. */
+#ifndef MPICH_API_PUBLIC
+#if defined(__GNUC__) || defined(__clang__)
+#define MPICH_API_PUBLIC __attribute__((visibility("default")))
+#else
+#define MPICH_API_PUBLIC
+#endif
+#endif
+
 /* ---- handle types (mpi.h.in:104,310) ---------------------------------- */
 typedef int MPI_Datatype;
 typedef int MPI_Op;
@@ -141,8 +153,8 @@ typedef void (MPI_User_function) (void *invec, void *inoutvec, int *len, MPI_Dat
  * i in [0,count).  Buffers may be HIP device memory, pinned host memory or
  * pageable host memory, in any combination; the combine always runs on the
  * GPU.  Synchronous: the result is complete in inoutbuf on return. */
-int MPI_Reduce_local(const void *inbuf, void *inoutbuf, int count, MPI_Datatype datatype, MPI_Op op);
-int PMPI_Reduce_local(const void *inbuf, void *inoutbuf, int count, MPI_Datatype datatype, MPI_Op op);
+MPICH_API_PUBLIC int MPI_Reduce_local(const void *inbuf, void *inoutbuf, int count, MPI_Datatype datatype, MPI_Op op);
+MPICH_API_PUBLIC int PMPI_Reduce_local(const void *inbuf, void *inoutbuf, int count, MPI_Datatype datatype, MPI_Op op);
 
 /* MPIR_Reduce_local (reduce_local.c:35): no argument validation; builtin ops
  * dispatch through MPIR_Op_table[op & 0xf], user ops through their function. */
@@ -187,18 +199,18 @@ extern MPIR_Op_check_dtype_fn *MPIR_Op_check_dtype_table[MPIR_OP_N_BUILTIN];
 #define MPIR_OP_HDL_TO_DTYPE_FN(op) MPIR_Op_check_dtype_table[((op)&0xf)]
 
 /* ---- user ops (op_create.c, op_free.c, op_commutative.c) ------------- */
-int MPI_Op_create(MPI_User_function * user_fn, int commute, MPI_Op * op);
-int PMPI_Op_create(MPI_User_function * user_fn, int commute, MPI_Op * op);
-int MPI_Op_free(MPI_Op * op);
-int PMPI_Op_free(MPI_Op * op);
-int MPI_Op_commutative(MPI_Op op, int *commute);
-int PMPI_Op_commutative(MPI_Op op, int *commute);
+MPICH_API_PUBLIC int MPI_Op_create(MPI_User_function * user_fn, int commute, MPI_Op * op);
+MPICH_API_PUBLIC int PMPI_Op_create(MPI_User_function * user_fn, int commute, MPI_Op * op);
+MPICH_API_PUBLIC int MPI_Op_free(MPI_Op * op);
+MPICH_API_PUBLIC int PMPI_Op_free(MPI_Op * op);
+MPICH_API_PUBLIC int MPI_Op_commutative(MPI_Op op, int *commute);
+MPICH_API_PUBLIC int PMPI_Op_commutative(MPI_Op op, int *commute);
 int MPIR_Op_is_commutative(MPI_Op op);
 
 /* ---- errors ------------------------------------------------------------ */
 #define MPI_MAX_ERROR_STRING 512
-int MPI_Error_class(int errorcode, int *errorclass);
-int MPI_Error_string(int errorcode, char *string, int *resultlen);
+MPICH_API_PUBLIC int MPI_Error_class(int errorcode, int *errorclass);
+MPICH_API_PUBLIC int MPI_Error_string(int errorcode, char *string, int *resultlen);
 
 /* ---- extensions -------------------------------------------------------- */
 /* Stream-ordered variant: enqueue the combine on `hip_stream` (a hipStream_t,
@@ -206,7 +218,7 @@ int MPI_Error_string(int errorcode, char *string, int *resultlen);
  * Both buffers must be device-accessible (hipMalloc / managed / mapped);
  * host-only pointers give MPI_ERR_BUFFER.  Same validation and error classes
  * as MPI_Reduce_local; user ops give MPI_ERR_OP (they run on the host). */
-int MPIX_Reduce_local_stream(const void *inbuf, void *inoutbuf, int count, MPI_Datatype datatype,
+MPICH_API_PUBLIC int MPIX_Reduce_local_stream(const void *inbuf, void *inoutbuf, int count, MPI_Datatype datatype,
                              MPI_Op op, void *hip_stream);
 /* Multi-operand local reduction: outbuf = fold of n device buffers in ONE pass
  * over HBM, in the association a reduction schedule would produce by calling
@@ -221,10 +233,10 @@ int MPIX_Reduce_local_stream(const void *inbuf, void *inoutbuf, int count, MPI_D
  * the same validation as MPI_Reduce_local. */
 #define MPIX_ORDER_TREE  0
 #define MPIX_ORDER_CHAIN 1
-int MPIX_Reduce_local_multi(const void *const *inbufs, int n, void *outbuf, int count,
+MPICH_API_PUBLIC int MPIX_Reduce_local_multi(const void *const *inbufs, int n, void *outbuf, int count,
                             MPI_Datatype datatype, MPI_Op op, int order, void *hip_stream);
-int MPIX_Reduce_local_set_errhandler(MPI_Errhandler errhandler);
-int MPIX_Reduce_local_get_errhandler(MPI_Errhandler * errhandler);
+MPICH_API_PUBLIC int MPIX_Reduce_local_set_errhandler(MPI_Errhandler errhandler);
+MPICH_API_PUBLIC int MPIX_Reduce_local_get_errhandler(MPI_Errhandler * errhandler);
 
 #ifdef __cplusplus
 }

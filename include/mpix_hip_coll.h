@@ -50,32 +50,32 @@ typedef struct MPIX_Hip_comm_s *MPIX_Hip_comm;
 #define MPIX_HIP_ALG_REFERENCE_ORDER 1
 #define MPIX_HIP_ALG_RCCL 2
 
-int MPIX_Hip_comm_get_unique_id(void *id);
-int MPIX_Hip_comm_create(const void *id, int size, int rank, MPIX_Hip_comm * comm);
-int MPIX_Hip_comm_create_loopback(int size, MPIX_Hip_comm * comms);
-int MPIX_Hip_comm_free(MPIX_Hip_comm * comm);
-int MPIX_Hip_comm_rank(MPIX_Hip_comm comm, int *rank);
-int MPIX_Hip_comm_size(MPIX_Hip_comm comm, int *size);
+MPICH_API_PUBLIC int MPIX_Hip_comm_get_unique_id(void *id);
+MPICH_API_PUBLIC int MPIX_Hip_comm_create(const void *id, int size, int rank, MPIX_Hip_comm * comm);
+MPICH_API_PUBLIC int MPIX_Hip_comm_create_loopback(int size, MPIX_Hip_comm * comms);
+MPICH_API_PUBLIC int MPIX_Hip_comm_free(MPIX_Hip_comm * comm);
+MPICH_API_PUBLIC int MPIX_Hip_comm_rank(MPIX_Hip_comm comm, int *rank);
+MPICH_API_PUBLIC int MPIX_Hip_comm_size(MPIX_Hip_comm comm, int *size);
 
 /* MPI_Allreduce semantics (sendbuf may be MPI_IN_PLACE). */
-int MPIX_Allreduce_hip(const void *sendbuf, void *recvbuf, int count, MPI_Datatype datatype, MPI_Op op,
+MPICH_API_PUBLIC int MPIX_Allreduce_hip(const void *sendbuf, void *recvbuf, int count, MPI_Datatype datatype, MPI_Op op,
                        MPIX_Hip_comm comm, int algorithm, void *hip_stream);
 /* MPI_Reduce semantics (reduce.c:382; MPI_IN_PLACE at the root only; recvbuf
  * significant at the root only).  Reference order: reduce_intra_smp.c ->
  * MPIR_Reduce_intra_auto on the node (binomial tree rooted at `root` for
  * count*size <= 2048 or count < pof2, else reduce-scatter + gather);
  * MPIX_HIP_ALG_RCCL: ncclReduce. */
-int MPIX_Reduce_hip(const void *sendbuf, void *recvbuf, int count, MPI_Datatype datatype, MPI_Op op, int root,
+MPICH_API_PUBLIC int MPIX_Reduce_hip(const void *sendbuf, void *recvbuf, int count, MPI_Datatype datatype, MPI_Op op, int root,
                     MPIX_Hip_comm comm, int algorithm, void *hip_stream);
 /* MPI_Reduce_scatter_block semantics (sendbuf may be MPI_IN_PLACE). */
-int MPIX_Reduce_scatter_block_hip(const void *sendbuf, void *recvbuf, int recvcount, MPI_Datatype datatype,
+MPICH_API_PUBLIC int MPIX_Reduce_scatter_block_hip(const void *sendbuf, void *recvbuf, int recvcount, MPI_Datatype datatype,
                                   MPI_Op op, MPIX_Hip_comm comm, int algorithm, void *hip_stream);
 /* MPI_Reduce_scatter semantics (reduce_scatter.c:383; rank q receives
  * recvcounts[q] elements; sendbuf may be MPI_IN_PLACE).  Reference order:
  * MPIR_Reduce_scatter_intra_auto (recursive halving below 524288 total bytes,
  * else pairwise); MPIX_HIP_ALG_RCCL: ncclReduceScatter when the counts are
  * all equal, else the reference order. */
-int MPIX_Reduce_scatter_hip(const void *sendbuf, void *recvbuf, const int recvcounts[], MPI_Datatype datatype,
+MPICH_API_PUBLIC int MPIX_Reduce_scatter_hip(const void *sendbuf, void *recvbuf, const int recvcounts[], MPI_Datatype datatype,
                             MPI_Op op, MPIX_Hip_comm comm, int algorithm, void *hip_stream);
 
 /* MPI_Scan / MPI_Exscan semantics (scan.c, exscan.c; sendbuf may be
@@ -83,9 +83,9 @@ int MPIX_Reduce_scatter_hip(const void *sendbuf, void *recvbuf, const int recvco
  * order of the recursive doubling (scan_intra_recursive_doubling.c,
  * exscan_intra_recursive_doubling.c); RCCL has no scan, so every algorithm
  * value runs the reference order. */
-int MPIX_Scan_hip(const void *sendbuf, void *recvbuf, int count, MPI_Datatype datatype, MPI_Op op,
+MPICH_API_PUBLIC int MPIX_Scan_hip(const void *sendbuf, void *recvbuf, int count, MPI_Datatype datatype, MPI_Op op,
                   MPIX_Hip_comm comm, int algorithm, void *hip_stream);
-int MPIX_Exscan_hip(const void *sendbuf, void *recvbuf, int count, MPI_Datatype datatype, MPI_Op op,
+MPICH_API_PUBLIC int MPIX_Exscan_hip(const void *sendbuf, void *recvbuf, int count, MPI_Datatype datatype, MPI_Op op,
                     MPIX_Hip_comm comm, int algorithm, void *hip_stream);
 
 #ifdef __cplusplus

@@ -53,9 +53,24 @@ int *MPIR_Op_errno_ptr(void);
 /* record a HIP runtime failure inside an op kernel (sets op_errno) */
 void MPIR_Op_report_hip_error(const char *opname, int hip_rc);
 
-/* the MPI-level error exit shared by every entry point: applies the
- * MPIX_Reduce_local errhandler (fatal by default) and returns the class */
-int MPIR_Err_return(const char *fcname, int mpi_errno);
+/* MPICH's error interface (src/mpi/errhan/errutil.c:238,848): weak
+ * standalone definitions in errutil.c, libmpi's own when linked into MPICH */
+#define MPIR_ERR_RECOVERABLE 0
+#define MPIR_ERR_FATAL 1
+int MPIR_Err_create_code(int lastcode, int fatal, const char fcname[], int line, int error_class,
+                         const char generic_msg[], const char specific_msg[], ...);
+int MPIR_Err_return_comm(void *comm_ptr, const char fcname[], int errcode);
+
+/* the MPI-level error exit shared by the entry points: the thread's detail
+ * text becomes the innermost error-stack level, then
+ * MPIR_Err_return_comm(NULL, ...) applies COMM_WORLD's handler (fatal by
+ * default) and returns the code (MPI_Error_class(code) is the class) */
+int MPIR_Err_wrap_detail(const char *fcname, int line, int mpi_errno);
+
+/* PMPI_Reduce_local's body (validation, MPIR_Reduce_local, error exit) */
+int MPIR_Reduce_local_checked(const void *inbuf, void *inoutbuf, int count, MPI_Datatype datatype, MPI_Op op);
+int MPIR_Err_return_at(const char *fcname, int line, int mpi_errno);
+#define MPIR_Err_return(fc, e) MPIR_Err_return_at((fc), __LINE__, (e))
 
 /* last error detail text for this thread (for MPI_Error_string) */
 const char *MPIR_Err_last_detail(void);

@@ -24,140 +24,80 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include "mpir_op_objects.h"
 #include "mpir_op_types.h"
 
-/* ---- handle layout (src/include/mpir_objects.h:150,163-205) ------------ */
-#define HANDLE_KIND_INVALID  0x0
-#define HANDLE_KIND_BUILTIN  0x1
-#define HANDLE_KIND_DIRECT   0x2
-#define HANDLE_KIND_INDIRECT 0x3
-#define HANDLE_GET_KIND(a)     (((unsigned)(a) & 0xc0000000u) >> 30)
-#define HANDLE_GET_MPI_KIND(a) (((unsigned)(a) & 0x3c000000u) >> 26)
-#define MPIR_OP_OBJ_KIND 0x6
+/* ---- handles and user ops: the MPIR_Op object store (op_objects.c) ----- */
+#define HANDLE_KIND_INVALID  MPIR_HANDLE_KIND_INVALID
+#define HANDLE_KIND_BUILTIN  MPIR_HANDLE_KIND_BUILTIN
+#define HANDLE_GET_KIND(a)     MPIR_HANDLE_GET_KIND(a)
+#define HANDLE_GET_MPI_KIND(a) MPIR_HANDLE_GET_MPI_KIND(a)
 
-/* ---- user op objects (op_create.c:73-104) ------------------------------ */
-#define MPIR_OP_KIND__USER_NONCOMMUTE 32
-#define MPIR_OP_KIND__USER 33
-#define MAX_USER_OPS 4096
-#define OP_PREALLOC 16          /* MPIR_OP_PREALLOC (op_create.c:27) */
-
-typedef struct {
-    int in_use;
-    int kind;
-    MPI_User_function *fn;
-} user_op_t;
-
-static user_op_t user_ops[MAX_USER_OPS];
-static pthread_mutex_t user_ops_lock = PTHREAD_MUTEX_INITIALIZER;
-
-/* direct handles 0x98000000|i for the first 16 objects, indirect
- * 0xd8000000|(block<<12)|index beyond (mpir_objects.h:183-205) */
-static MPI_Op user_op_handle(int slot)
+/* A live user-defined op: MPIR_Op_get_ptr + MPIR_Op_valid_ptr
+ * (reduce_local.c:172-177), plus a check the reference does not make --
+ * that the object is allocated (its handle is this handle, its reference
+ * count positive) -- so a freed or never-created handle returns
+ * MPI_ERR_OP instead of calling through a stale function pointer. */
+static MPIR_Op *user_op_get(MPI_Op op)
 {
-    if (slot < OP_PREALLOC)
-        return (MPI_Op) (0x98000000u | (unsigned) slot);
-    slot -= OP_PREALLOC;
-    return (MPI_Op) (0xd8000000u | ((unsigned) (slot / 1024) << 12) | (unsigned) (slot % 1024));
-}
-
-static user_op_t *user_op_get(MPI_Op op)
-{
-    unsigned h = (unsigned) op;
-    int slot;
-    if (HANDLE_GET_MPI_KIND(h) != MPIR_OP_OBJ_KIND)
+    MPIR_Op *p;
+    if (HANDLE_GET_MPI_KIND(op) != MPIR_OP_OBJ_KIND || HANDLE_GET_KIND(op) == HANDLE_KIND_BUILTIN)
         return NULL;
-    if (HANDLE_GET_KIND(h) == HANDLE_KIND_DIRECT) {
-        slot = (int) (h & 0x03ffffffu);
-        if (slot >= OP_PREALLOC)
-            return NULL;
-    } else if (HANDLE_GET_KIND(h) == HANDLE_KIND_INDIRECT) {
-        slot = OP_PREALLOC + (int) (((h & 0x03fff000u) >> 12) * 1024 + (h & 0xfffu));
-        if (slot >= MAX_USER_OPS)
-            return NULL;
-    } else {
+    p = MPIR_Op_get_ptr_fn(op);
+    if (!p || p->handle != op || __atomic_load_n(&p->ref_count, __ATOMIC_ACQUIRE) <= 0 ||
+        p->kind < MPIR_OP_KIND__USER_NONCOMMUTE)
         return NULL;
-    }
-    return user_ops[slot].in_use ? &user_ops[slot] : NULL;
+    return p;
 }
 
 /* ---- error handling ----------------------------------------------------- */
-static MPI_Errhandler reduce_local_errhandler = MPI_ERRORS_ARE_FATAL;
+/* COMM_WORLD's handler as MPIR_Err_return_comm(NULL, ...) sees it: fatal,
+ * unless MPIR_CVAR_REDUCE_LOCAL_ERRHANDLER=return (for the LD_PRELOAD shim,
+ * whose MPIX_ setter the application cannot reach) or the setter says so */
+static MPI_Errhandler reduce_local_errhandler = 0;
 
-static const char *class_string(int cls)
+static MPI_Errhandler default_errhandler(void)
 {
-    switch (cls) {
-    case MPI_SUCCESS:
-        return "No MPI error";
-    case MPI_ERR_BUFFER:
-        return "Invalid buffer pointer";
-    case MPI_ERR_COUNT:
-        return "Invalid count";
-    case MPI_ERR_TYPE:
-        return "Invalid datatype";
-    case 5:     /* MPI_ERR_COMM */
-        return "Invalid communicator";
-    case 7:     /* MPI_ERR_ROOT */
-        return "Invalid root";
-    case MPI_ERR_OP:
-        return "Invalid MPI_Op";
-    case MPI_ERR_ARG:
-        return "Invalid argument";
-    case MPI_ERR_OTHER:
-        return "Other MPI error";
-    case MPI_ERR_INTERN:
-        return "Internal MPI error!";
-    case MPI_ERR_NO_MEM:
-        return "Out of memory";
-    default:
-        return "Unknown error class";
-    }
-}
-
-int MPI_Error_class(int errorcode, int *errorclass)
-{
-    *errorclass = errorcode & 0x7f;     /* ERROR_CLASS_MASK (dynerrutil.c:40) */
-    return MPI_SUCCESS;
-}
-
-int MPI_Error_string(int errorcode, char *string, int *resultlen)
-{
-    const char *detail = MPIR_Err_last_detail();
-    int n;
-    if (errorcode != MPI_SUCCESS && detail[0])
-        n = snprintf(string, MPI_MAX_ERROR_STRING, "%s, error stack:\n%s",
-                     class_string(errorcode & 0x7f), detail);
-    else
-        n = snprintf(string, MPI_MAX_ERROR_STRING, "%s", class_string(errorcode & 0x7f));
-    if (n >= MPI_MAX_ERROR_STRING)
-        n = MPI_MAX_ERROR_STRING - 1;
-    *resultlen = n;
-    return MPI_SUCCESS;
+    const char *e = getenv("MPIR_CVAR_REDUCE_LOCAL_ERRHANDLER");
+    return (e && !strcmp(e, "return")) ? MPI_ERRORS_RETURN : MPI_ERRORS_ARE_FATAL;
 }
 
 int MPIX_Reduce_local_set_errhandler(MPI_Errhandler errhandler)
 {
     if (errhandler != MPI_ERRORS_ARE_FATAL && errhandler != MPI_ERRORS_RETURN)
         return MPI_ERR_ARG;
-    reduce_local_errhandler = errhandler;
+    __atomic_store_n(&reduce_local_errhandler, errhandler, __ATOMIC_RELAXED);
     return MPI_SUCCESS;
 }
 
 int MPIX_Reduce_local_get_errhandler(MPI_Errhandler * errhandler)
 {
-    *errhandler = reduce_local_errhandler;
+    MPI_Errhandler h = __atomic_load_n(&reduce_local_errhandler, __ATOMIC_RELAXED);
+    *errhandler = h ? h : default_errhandler();
     return MPI_SUCCESS;
 }
 
-/* MPIR_Err_return_comm(NULL, fcname, errcode) (errutil.c:238) */
-int MPIR_Err_return(const char *fcname, int mpi_errno)
+/* The innermost level of an error stack: a bare class raised inside this
+ * library (its text in the thread's detail slot) becomes an MPICH error code
+ * (MPIR_Err_create_code, errutil.c here or libmpi's own).  A code that already
+ * carries a stack passes through. */
+int MPIR_Err_wrap_detail(const char *fcname, int line, int mpi_errno)
 {
-    if (reduce_local_errhandler == MPI_ERRORS_ARE_FATAL) {
-        fprintf(stderr, "Fatal error in %s: %s, error stack:\n%s: %s\n", fcname,
-                class_string(mpi_errno & 0x7f), fcname, MPIR_Err_last_detail());
-        fflush(stderr);
-        exit(1);
-    }
-    return mpi_errno;
+    const char *detail;
+    if (mpi_errno == MPI_SUCCESS || (mpi_errno & ~0x7f) != 0)
+        return mpi_errno;
+    detail = MPIR_Err_last_detail();
+    if (!detail[0])
+        return MPIR_Err_create_code(MPI_SUCCESS, MPIR_ERR_RECOVERABLE, fcname, line, mpi_errno, "**other", NULL);
+    return MPIR_Err_create_code(MPI_SUCCESS, MPIR_ERR_RECOVERABLE, fcname, line, mpi_errno, "**other", "%s", detail);
+}
+
+/* The MPI-level error exit of every entry point but MPI_Reduce_local's own:
+ * wrap, then MPIR_Err_return_comm(NULL, ...) (errutil.c:238) -- COMM_WORLD's
+ * handler, fatal by default. */
+int MPIR_Err_return_at(const char *fcname, int line, int mpi_errno)
+{
+    return MPIR_Err_return_comm(NULL, fcname, MPIR_Err_wrap_detail(fcname, line, mpi_errno));
 }
 
 #define err_return MPIR_Err_return
@@ -194,10 +134,7 @@ static int validate(const void *inbuf, void *inoutbuf, int count, MPI_Datatype d
         return MPI_ERR_OP;
     }
     if (HANDLE_GET_KIND(op) != HANDLE_KIND_BUILTIN) {
-        pthread_mutex_lock(&user_ops_lock);
-        user_op_t *u = user_op_get(op);
-        pthread_mutex_unlock(&user_ops_lock);
-        if (!u) {       /* MPIR_Op_valid_ptr */
+        if (!user_op_get(op)) {         /* MPIR_Op_valid_ptr */
             MPIR_Err_set_detail("Invalid MPI_Op");
             return MPI_ERR_OP;
         }
@@ -293,11 +230,9 @@ int MPIR_Reduce_local(const void *inbuf, void *inoutbuf, int count, MPI_Datatype
         }
         (*uop) ((void *) inbuf, inoutbuf, &count, &datatype);
     } else {
-        user_op_t *u;
-        pthread_mutex_lock(&user_ops_lock);
-        u = user_op_get(op);
-        uop = u ? u->fn : NULL;
-        pthread_mutex_unlock(&user_ops_lock);
+        /* MPIR_Op_get_ptr; a C-language op calls function.c_function (:65-82) */
+        MPIR_Op *op_ptr = user_op_get(op);
+        uop = op_ptr ? (MPI_User_function *) op_ptr->function.c_function : NULL;
         if (!uop) {
             MPIR_Err_set_detail("Invalid MPI_Op");
             return MPI_ERR_OP;
@@ -313,19 +248,35 @@ int MPIR_Reduce_local(const void *inbuf, void *inoutbuf, int count, MPI_Datatype
 }
 
 /* ---- MPI_Reduce_local (reduce_local.c:155-219) -------------------------- */
-int PMPI_Reduce_local(const void *inbuf, void *inoutbuf, int count, MPI_Datatype datatype, MPI_Op op)
+/* The body of PMPI_Reduce_local, under an internal name the LD_PRELOAD shim
+ * (preload.c) also calls. */
+int MPIR_Reduce_local_checked(const void *inbuf, void *inoutbuf, int count, MPI_Datatype datatype, MPI_Op op)
 {
+    static const char FCNAME[] = "PMPI_Reduce_local";
     int mpi_errno = validate(inbuf, inoutbuf, count, datatype, op);
     if (mpi_errno == MPI_SUCCESS)
         mpi_errno = MPIR_Reduce_local(inbuf, inoutbuf, count, datatype, op);
-    if (mpi_errno != MPI_SUCCESS)
-        mpi_errno = err_return("PMPI_Reduce_local", mpi_errno);
+    if (mpi_errno != MPI_SUCCESS) {
+        /* fn_fail (reduce_local.c:208-217) */
+        mpi_errno = MPIR_Err_wrap_detail(FCNAME, __LINE__, mpi_errno);
+        mpi_errno = MPIR_Err_create_code(mpi_errno, MPIR_ERR_RECOVERABLE, FCNAME, __LINE__, MPI_ERR_OTHER,
+                                         "**mpi_reduce_local", "**mpi_reduce_local %p %p %d %D %O", inbuf,
+                                         inoutbuf, count, datatype, op);
+        mpi_errno = MPIR_Err_return_comm(NULL, FCNAME, mpi_errno);
+    }
     return mpi_errno;
+}
+
+#ifndef MPIR_PRELOAD_SHIM
+int PMPI_Reduce_local(const void *inbuf, void *inoutbuf, int count, MPI_Datatype datatype, MPI_Op op)
+{
+    return MPIR_Reduce_local_checked(inbuf, inoutbuf, count, datatype, op);
 }
 
 /* profiling interface: MPI_ is a weak alias of PMPI_ (reduce_local.c:10-20) */
 int MPI_Reduce_local(const void *inbuf, void *inoutbuf, int count, MPI_Datatype datatype, MPI_Op op)
     __attribute__ ((weak, alias("PMPI_Reduce_local")));
+#endif
 
 /* ---- MPIX_Reduce_local_stream: enqueue on a HIP stream, no wait -------- */
 int MPIX_Reduce_local_stream(const void *inbuf, void *inoutbuf, int count, MPI_Datatype datatype,
@@ -407,80 +358,57 @@ int MPIX_Reduce_local_multi(const void *const *inbufs, int n, void *outbuf, int 
 /* ---- MPI_Op_create / MPI_Op_free / MPI_Op_commutative ------------------ */
 int PMPI_Op_create(MPI_User_function * user_fn, int commute, MPI_Op * op)
 {
-    int slot;
-    pthread_mutex_lock(&user_ops_lock);
-    for (slot = 0; slot < MAX_USER_OPS; slot++)
-        if (!user_ops[slot].in_use)
-            break;
-    if (slot == MAX_USER_OPS) {
-        pthread_mutex_unlock(&user_ops_lock);
-        MPIR_Err_set_detail("Out of memory (MPI_Op)");
-        return MPI_ERR_OTHER;   /* op_create.c:80-86 "**nomem" */
-    }
-    user_ops[slot].in_use = 1;
-    user_ops[slot].kind = commute ? MPIR_OP_KIND__USER : MPIR_OP_KIND__USER_NONCOMMUTE;
-    user_ops[slot].fn = user_fn;
-    pthread_mutex_unlock(&user_ops_lock);
-    *op = user_op_handle(slot);
+    int mpi_errno = MPIR_Op_create_impl(user_fn, commute, op);
+    if (mpi_errno != MPI_SUCCESS)
+        return err_return("PMPI_Op_create", mpi_errno);
     return MPI_SUCCESS;
 }
 
 int MPI_Op_create(MPI_User_function * user_fn, int commute, MPI_Op * op)
     __attribute__ ((weak, alias("PMPI_Op_create")));
 
+/* op_free.c:79-122: a predefined op is "**permop" */
 int PMPI_Op_free(MPI_Op * op)
 {
-    user_op_t *u;
-    pthread_mutex_lock(&user_ops_lock);
-    u = user_op_get(*op);
-    if (!u) {
-        pthread_mutex_unlock(&user_ops_lock);
-        if (HANDLE_GET_KIND(*op) == HANDLE_KIND_BUILTIN && HANDLE_GET_MPI_KIND(*op) == MPIR_OP_OBJ_KIND) {
-            MPIR_Err_set_detail("Cannot free permanent MPI_Op");       /* op_free.c "**permop" */
-            return err_return("PMPI_Op_free", MPI_ERR_OP);
-        }
+    if (HANDLE_GET_KIND(*op) == HANDLE_KIND_BUILTIN && HANDLE_GET_MPI_KIND(*op) == MPIR_OP_OBJ_KIND) {
+        MPIR_Err_set_detail("Cannot free permanent MPI_Op");       /* "**permop" */
+        return err_return("PMPI_Op_free", MPI_ERR_OP);
+    }
+    if (!user_op_get(*op)) {
         MPIR_Err_set_detail("Invalid MPI_Op");
         return err_return("PMPI_Op_free", MPI_ERR_OP);
     }
-    u->in_use = 0;
-    u->fn = NULL;
-    pthread_mutex_unlock(&user_ops_lock);
-    *op = MPI_OP_NULL;
+    MPIR_Op_free_impl(op);
     return MPI_SUCCESS;
 }
 
 int MPI_Op_free(MPI_Op * op) __attribute__ ((weak, alias("PMPI_Op_free")));
 
+/* op_commutative.c:39-53 */
 int MPIR_Op_is_commutative(MPI_Op op)
 {
-    user_op_t *u;
-    int kind;
+    MPIR_Op *op_ptr;
     if (HANDLE_GET_KIND(op) == HANDLE_KIND_BUILTIN)
         return 1;
-    pthread_mutex_lock(&user_ops_lock);
-    u = user_op_get(op);
-    kind = u ? u->kind : MPIR_OP_KIND__USER;
-    pthread_mutex_unlock(&user_ops_lock);
-    return kind == MPIR_OP_KIND__USER_NONCOMMUTE ? 0 : 1;
+    op_ptr = MPIR_Op_get_ptr_fn(op);
+    return !(op_ptr && op_ptr->kind == MPIR_OP_KIND__USER_NONCOMMUTE);
 }
 
+/* op_commutative.c:101-140 */
 int PMPI_Op_commutative(MPI_Op op, int *commute)
 {
+    MPIR_Op *op_ptr;
     if (HANDLE_GET_KIND(op) != HANDLE_KIND_BUILTIN) {
-        user_op_t *u;
-        pthread_mutex_lock(&user_ops_lock);
-        u = user_op_get(op);
-        pthread_mutex_unlock(&user_ops_lock);
-        if (!u) {
+        op_ptr = user_op_get(op);
+        if (!op_ptr) {
             MPIR_Err_set_detail("Invalid MPI_Op");
             return err_return("PMPI_Op_commutative", MPI_ERR_OP);
         }
-    } else if (HANDLE_GET_MPI_KIND(op) != MPIR_OP_OBJ_KIND) {
+    } else if (HANDLE_GET_MPI_KIND(op) != MPIR_OP_OBJ_KIND || !(op_ptr = MPIR_Op_get_ptr_fn(op))) {
         MPIR_Err_set_detail("Invalid MPI_Op");
         return err_return("PMPI_Op_commutative", MPI_ERR_OP);
     }
-    *commute = MPIR_Op_is_commutative(op);
-    return MPI_SUCCESS;
+    return MPIR_Op_commutative(op_ptr, commute);
 }
 
 int MPI_Op_commutative(MPI_Op op, int *commute) __attribute__ ((weak, alias("PMPI_Op_commutative")));

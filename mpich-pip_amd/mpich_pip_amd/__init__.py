@@ -196,6 +196,14 @@ def load(path: str | None = None) -> ctypes.CDLL:
     return lib
 
 
+def error_class(code: int) -> int:
+    """MPI_Error_class: the class of an error code (codes carry an error-stack
+    index above the class bits, as MPICH's do)."""
+    c = ctypes.c_int(-1)
+    load().MPI_Error_class(code, ctypes.byref(c))
+    return c.value
+
+
 def error_string(code: int) -> str:
     lib = load()
     buf = ctypes.create_string_buffer(512)

@@ -84,11 +84,12 @@ int main(int argc, char **argv)
 
     /* error classes */
     {
-        int x = 0, y = 0;
-        printf("errs %d %d %d %d\n", MPI_Reduce(&x, &y, 1, MPI_INT, MPI_SUM, size, MPI_COMM_WORLD),
-               MPI_Bcast(&x, 1, MPI_INT, 0, (MPI_Comm) 0x44000007),
-               MPI_Reduce(&x, &y, -1, MPI_INT, MPI_SUM, 0, MPI_COMM_WORLD),
-               MPI_Reduce(&x, &y, 1, MPI_BYTE, MPI_SUM, 0, MPI_COMM_WORLD));
+        int x = 0, y = 0, c[4];
+        MPI_Error_class(MPI_Reduce(&x, &y, 1, MPI_INT, MPI_SUM, size, MPI_COMM_WORLD), &c[0]);
+        MPI_Error_class(MPI_Bcast(&x, 1, MPI_INT, 0, (MPI_Comm) 0x44000007), &c[1]);
+        MPI_Error_class(MPI_Reduce(&x, &y, -1, MPI_INT, MPI_SUM, 0, MPI_COMM_WORLD), &c[2]);
+        MPI_Error_class(MPI_Reduce(&x, &y, 1, MPI_BYTE, MPI_SUM, 0, MPI_COMM_WORLD), &c[3]);
+        printf("errs %d %d %d %d\n", c[0], c[1], c[2], c[3]);
     }
 
     if (gpu) {

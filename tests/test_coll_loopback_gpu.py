@@ -376,12 +376,16 @@ def test_collective_validation(mpi, cuda):
     a = torch.zeros(16, device="cuda")
     b = torch.zeros(16, device="cuda")
     try:
-        assert mpi.allreduce(a.data_ptr(), b.data_ptr(), 16, mpi.MPI_FLOAT, mpi.MPI_LAND, comms[0]) == mpi.MPI_ERR_OP
-        assert mpi.allreduce(a.data_ptr(), a.data_ptr(), 16, mpi.MPI_FLOAT, mpi.MPI_SUM, comms[0]) == mpi.MPI_ERR_BUFFER
-        assert mpi.allreduce(a.data_ptr(), b.data_ptr(), -1, mpi.MPI_FLOAT, mpi.MPI_SUM, comms[0]) == mpi.MPI_ERR_COUNT
-        assert mpi.allreduce(a.data_ptr(), b.data_ptr(), 16, mpi.MPI_FLOAT, mpi.MPI_REPLACE, comms[0]) == mpi.MPI_ERR_OP
-        assert mpi.reduce_scatter_block(a.data_ptr(), b.data_ptr(), 16, mpi.MPI_BYTE, mpi.MPI_SUM,
-                                        comms[0]) == mpi.MPI_ERR_OP
+        ec = mpi.error_class
+        assert ec(mpi.allreduce(a.data_ptr(), b.data_ptr(), 16, mpi.MPI_FLOAT, mpi.MPI_LAND, comms[0])) == mpi.MPI_ERR_OP
+        assert ec(mpi.allreduce(a.data_ptr(), a.data_ptr(), 16, mpi.MPI_FLOAT, mpi.MPI_SUM, comms[0])) == \
+            mpi.MPI_ERR_BUFFER
+        assert ec(mpi.allreduce(a.data_ptr(), b.data_ptr(), -1, mpi.MPI_FLOAT, mpi.MPI_SUM, comms[0])) == \
+            mpi.MPI_ERR_COUNT
+        assert ec(mpi.allreduce(a.data_ptr(), b.data_ptr(), 16, mpi.MPI_FLOAT, mpi.MPI_REPLACE, comms[0])) == \
+            mpi.MPI_ERR_OP
+        assert ec(mpi.reduce_scatter_block(a.data_ptr(), b.data_ptr(), 16, mpi.MPI_BYTE, mpi.MPI_SUM,
+                                           comms[0])) == mpi.MPI_ERR_OP
         assert mpi.allreduce(a.data_ptr(), b.data_ptr(), 0, mpi.MPI_FLOAT, mpi.MPI_SUM, comms[0]) == 0
     finally:
         mpi.comm_free(comms[0])

@@ -221,9 +221,10 @@ def test_stream_variant(mpi, orc, cuda):
     assert np.array_equal(back(tio, 0, a.size), want)
     # host pointers are refused by the stream variant
     h = np.zeros(16, np.float32)
-    assert mpi.reduce_local_stream(h.ctypes.data, pio, 4, mpi.MPI_FLOAT, mpi.MPI_SUM, 0) == mpi.MPI_ERR_BUFFER
+    assert mpi.error_class(mpi.reduce_local_stream(h.ctypes.data, pio, 4, mpi.MPI_FLOAT, mpi.MPI_SUM, 0)) == \
+        mpi.MPI_ERR_BUFFER
     # float LAND passes check_dtype then fails in the compute switch (op_errno)
-    assert mpi.reduce_local_stream(pin, pio, 4, mpi.MPI_FLOAT, mpi.MPI_LAND, 0) == mpi.MPI_ERR_OP
+    assert mpi.error_class(mpi.reduce_local_stream(pin, pio, 4, mpi.MPI_FLOAT, mpi.MPI_LAND, 0)) == mpi.MPI_ERR_OP
 
 
 def test_stream_variant_in_hip_graph(mpi, orc, cuda):
@@ -466,7 +467,8 @@ def test_concurrent_host_threads(mpi, orc, cuda):
         if rc:
             errs.append(rc)
         # an invalid call on the same thread must not disturb the others
-        if mpi.reduce_local(db.data_ptr(), da.data_ptr(), n, mpi.MPI_DOUBLE, mpi.MPI_BAND) != mpi.MPI_ERR_OP:
+        if mpi.error_class(mpi.reduce_local(db.data_ptr(), da.data_ptr(), n, mpi.MPI_DOUBLE, mpi.MPI_BAND)) != \
+                mpi.MPI_ERR_OP:
             errs.append("band")
 
     ths = [threading.Thread(target=work, args=(i,)) for i in range(8)]
@@ -511,7 +513,8 @@ def test_thread_contexts_reused(mpi, cuda):
 
 
 def test_concurrent_pageable_threads(mpi, orc, cuda):
-    """Four host threads reduce pageable host buffers at once: each has its own
+    """Four host threads reduce pageable host buffers at once (the binding
+    releases the GIL around the call): each has its own
     staging streams and bounce slots, and they share the copy pool (one split
     copy at a time); every result bit-exact."""
     import threading
@@ -524,13 +527,14 @@ def test_concurrent_pageable_threads(mpi, orc, cuda):
         data.append((a, b, a + b, a.copy()))  # one IEEE add per element, as the reference
     errs = []
 
+    fast = mpi.fast_reduce_local()
+
     def work(i):
+        # all four through the compiled binding, which releases the GIL for the
+        # call, so the four really overlap
         a, b, _, a0 = data[i]
         for rep in range(2):
-            if i % 2:
-                rc = mpi.reduce_local(b.ctypes.data, a.ctypes.data, n, mpi.MPI_FLOAT, mpi.MPI_SUM)
-            else:
-                rc = mpi.fast_reduce_local()(b.ctypes.data, a.ctypes.data, n, mpi.MPI_FLOAT, mpi.MPI_SUM)
+            rc = fast(b.ctypes.data, a.ctypes.data, n, mpi.MPI_FLOAT, mpi.MPI_SUM)
             if rc:
                 errs.append((i, rc))
             if rep == 0:

@@ -117,14 +117,15 @@ def test_multi_validation(mpi, cuda):
     b = torch.zeros(64, device="cuda")
     ptrs = [a.data_ptr(), b.data_ptr(), a.data_ptr()]
     # tree needs a power of two
-    assert mpi.reduce_local_multi(ptrs, b.data_ptr(), 64, mpi.MPI_FLOAT, mpi.MPI_SUM,
-                                  mpi.MPIX_ORDER_TREE) == mpi.MPI_ERR_ARG
+    ec = mpi.error_class
+    assert ec(mpi.reduce_local_multi(ptrs, b.data_ptr(), 64, mpi.MPI_FLOAT, mpi.MPI_SUM,
+                                     mpi.MPIX_ORDER_TREE)) == mpi.MPI_ERR_ARG
     # op/type check like MPI_Reduce_local
-    assert mpi.reduce_local_multi(ptrs[:2], b.data_ptr(), 64, mpi.MPI_FLOAT, mpi.MPI_BAND,
-                                  mpi.MPIX_ORDER_CHAIN) == mpi.MPI_ERR_OP
+    assert ec(mpi.reduce_local_multi(ptrs[:2], b.data_ptr(), 64, mpi.MPI_FLOAT, mpi.MPI_BAND,
+                                     mpi.MPIX_ORDER_CHAIN)) == mpi.MPI_ERR_OP
     h = np.zeros(64, np.float32)
-    assert mpi.reduce_local_multi([h.ctypes.data, a.data_ptr()], b.data_ptr(), 64, mpi.MPI_FLOAT, mpi.MPI_SUM,
-                                  mpi.MPIX_ORDER_CHAIN) == mpi.MPI_ERR_BUFFER
+    assert ec(mpi.reduce_local_multi([h.ctypes.data, a.data_ptr()], b.data_ptr(), 64, mpi.MPI_FLOAT, mpi.MPI_SUM,
+                                     mpi.MPIX_ORDER_CHAIN)) == mpi.MPI_ERR_BUFFER
 
 
 ANY = [("MPI_DOUBLE_INT", "MPI_MINLOC"), ("MPI_2INT", "MPI_MAXLOC"), ("MPI_INT", "MPI_LAND"),
