@@ -26,8 +26,9 @@ Extra fields (rank 0):
   pcie_inclusive  pinned host buffers -> MPI_Reduce_local (H2D + kernel + D2H),
                 the rate when rank buffers arrive in host memory over PiP shm.
                 Reported for DESIGN.md; never `value`.
-  cpu_baseline  the oracle's C loop (reference algorithm, gcc -O2) timed on this
-                box's host cores on a bounded sample (rank 0, N = 1 only).
+  cpu_baseline  the oracle's C loop (reference algorithm, gcc -O2) timed on every
+                physical core of this box, one pinned thread per core with NUMA-local
+                operands, on a bounded sample (rank 0, N = 1 only); per socket too.
 """
 from __future__ import annotations
 
@@ -58,8 +59,7 @@ def parse():
     ap.add_argument("--mib", type=int, default=256, help="MiB per operand (metric: 256)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="only the timed MPI_Reduce_local loop")
-    ap.add_argument("--cpu-threads", type=int, default=0, help="cpu_baseline threads (0 = min(16, affinity))")
-    ap.add_argument("--cpu-iters", type=int, default=48)
+    ap.add_argument("--cpu-iters", type=int, default=24, help="cpu_baseline calls per thread")
     ap.add_argument("--collectives", choices=["auto", "on", "off"], default="auto",
                     help="configs 4-5 via bench_coll.py in isolated child processes (auto: when N > 1)")
     ap.add_argument("--cpu-standin", action="store_true",
@@ -258,18 +258,78 @@ def load_traffic(count_bytes: int):
     return d.get("hbm_bytes_per_launch"), os.path.relpath(p, ROOT)
 
 
-def host_cpu(affinity: int) -> str:
-    """CPU model and the core counts the baseline ran beside (record nproc/lscpu)."""
-    model = "unknown"
+def lscpu_topology() -> dict:
+    """The lines of `lscpu` that describe the host's cores."""
+    import subprocess
+    keys = ("Model name", "Socket(s)", "Core(s) per socket", "Thread(s) per core", "NUMA node(s)", "CPU(s)")
     try:
-        with open("/proc/cpuinfo") as f:
-            for ln in f:
-                if ln.startswith("model name"):
-                    model = ln.split(":", 1)[1].strip()
-                    break
-    except OSError:
-        pass
-    return f"{model}; {os.cpu_count()} logical CPUs on the host, {affinity} in this process's affinity"
+        txt = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=20).stdout
+    except (OSError, subprocess.SubprocessError):
+        return {}
+    out = {}
+    for ln in txt.splitlines():
+        k, _, v = ln.partition(":")
+        if k.strip() in keys and k.strip() not in out:
+            out[k.strip()] = v.strip()
+    return out
+
+
+def cpu_baseline(args, count: int, alg_bytes: int) -> dict:
+    """The reference's fp32 SUM loop (oracle/op_oracle.c, gcc -O2 like MPICH) on
+    the host cores this process may use: one thread pinned per physical core,
+    dealt over the sockets, each with its own NUMA-local (first-touched)
+    256 MiB operand pair, all started by one barrier; aggregate = all threads'
+    algorithmic bytes / slowest thread, per socket likewise.
+    "Usable" is the physical cores of the CPU affinity, capped by the cgroup
+    CPU quota: the GPU box shows 128 physical cores but grants 16 CPUs' worth of
+    time, and 128 threads under that quota run 1/8 of each period (measured:
+    130 GiB/s, against ~335 for 16 threads), a throttling figure, not a CPU
+    rate -- it is reported beside the main figure as `all_physical_cores`.
+    Also the clang -O2 build on the same cores."""
+    import oracle
+    machine = oracle.physical_cores()
+    quota = oracle.cpu_quota()
+    usable = min(len(machine), int(quota)) if quota else len(machine)
+    cores = oracle.spread_over_sockets(machine, max(1, usable))
+    iters = args.cpu_iters
+
+    def run(cs, per, its, compiler):
+        secs = oracle.cpu_baseline_pinned([c for c, _ in cs], per, its, compiler)
+        if min(secs) <= 0:
+            return None
+        bpt = 3 * per * 4 * its             # algorithmic bytes per thread
+        agg = bpt * len(cs) / max(secs) / GIB
+        sockets = {}
+        for (c, pkg), t in zip(cs, secs):
+            sockets.setdefault(pkg, []).append(t)
+        return {"value": round(agg, 2), "per_core": round(agg / len(cs), 2),
+                "per_socket": {str(k): round(bpt * len(v) / max(v) / GIB, 2) for k, v in sorted(sockets.items())},
+                "seconds": round(max(secs), 3)}
+
+    per = count - count % 64
+    g = run(cores, per, iters, "gcc")
+    if g is None:
+        return {"error": "cpu baseline thread failure"}
+    res = {"unit": "GiB/s", "kind": "port", "cores": len(cores)}
+    res.update(g)
+    res["sample"] = (f"{len(cores)} threads, one pinned per physical core (dealt over the sockets), {iters} calls each "
+                     f"of MPI_SUM MPI_FLOAT count {per} on its own first-touched 256 MiB (inbuf, inoutbuf) pair; "
+                     f"oracle/op_oracle.c SUM loop, gcc -O2 (MPICH's default build); aggregate = algorithmic bytes of "
+                     f"all threads / slowest thread")
+    res["machine"] = {"physical_cores": len(machine), "cgroup_cpu_quota": quota, "lscpu": lscpu_topology()}
+    try:
+        c = run(cores, per, iters, "clang")
+    except RuntimeError as e:
+        c = {"error": str(e)}
+    res["clang_O2"] = c if c is not None else {"error": "thread failure"}
+    if quota and len(machine) > usable:
+        small = int(min(count, (16 << 30) // (8 * len(machine))))
+        a = run(machine, small - small % 64, max(4, iters // 3), "gcc")
+        if a is not None:
+            a["note"] = (f"{len(machine)} pinned threads (count {small - small % 64} each) under the "
+                         f"{quota:g}-CPU cgroup quota: throttled, not a CPU rate")
+            res["all_physical_cores"] = a
+    return res
 
 
 def main():
@@ -443,35 +503,7 @@ def main():
             out["collectives"] = coll
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        import oracle
-        try:
-            aff = len(os.sched_getaffinity(0))
-        except AttributeError:
-            aff = os.cpu_count() or 1
-        threads = args.cpu_threads or max(1, min(16, aff))
-        secs = oracle.cpu_baseline_sum_f32(threads, count, args.cpu_iters)
-        if secs > 0:
-            cv = alg_bytes * args.cpu_iters * threads / secs / GIB
-            out["cpu_baseline"] = {
-                "value": round(cv, 2), "unit": "GiB/s", "cores": threads, "kind": "port",
-                "sample": f"{threads} threads x {args.cpu_iters} calls, each thread its own "
-                          f"{args.mib} MiB fp32 (inbuf, inoutbuf) pair; oracle/op_oracle.c SUM loop, gcc -O2",
-                "per_core": round(cv / threads, 2),
-                "seconds": round(secs, 3),
-                "host": host_cpu(aff),
-            }
-            # the same loop built with clang -O2 (SURVEY.md §8d asks for both compilers)
-            cerr = "thread failure"
-            try:
-                csecs = oracle.cpu_baseline_sum_f32(threads, count, args.cpu_iters, "clang")
-            except RuntimeError as e:
-                csecs, cerr = -1.0, str(e)
-            if csecs > 0:
-                ccv = alg_bytes * args.cpu_iters * threads / csecs / GIB
-                out["cpu_baseline"]["clang_O2"] = {"value": round(ccv, 2), "per_core": round(ccv / threads, 2),
-                                                   "seconds": round(csecs, 3)}
-            else:
-                out["cpu_baseline"]["clang_O2"] = {"error": cerr}
+        out["cpu_baseline"] = cpu_baseline(args, count, alg_bytes)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -15,6 +15,8 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <stdint.h>
+
 #include "mpir_op_types.h"
 
 /* ------------------------------------------------------------ type matrix */
@@ -227,20 +229,34 @@ DEFINE_OP(MPIR_BXOR, MPIR_HIP_OP_BXOR, "MPI_BXOR")
 DEFINE_OP(MPIR_MINLOC, MPIR_HIP_OP_MINLOC, "MPI_MINLOC")
 DEFINE_OP(MPIR_MAXLOC, MPIR_HIP_OP_MAXLOC, "MPI_MAXLOC")
 
-/* MPIR_REPLACE (opreplace.c:15): MPIR_Localcopy of len elements.  Only basic
- * types exist in this library, so the copy is count * size bytes. */
+/* MPIR_REPLACE (opreplace.c:15-18): MPIR_Localcopy(invec, len, type, inoutvec,
+ * len, type), reached through the table by RMA accumulate (mpidrma.h:902).
+ * Every predefined datatype is a contiguous copy of len * size bytes: the
+ * basic ones of this library's type table, and any other builtin-kind handle
+ * (MPI_WCHAR, MPI_PACKED, Fortran types, MPI_LB / MPI_UB of size 0) by the
+ * size its handle encodes in bits 8-15 (MPIR_Datatype_get_basic_size,
+ * mpir_datatype.h:172).  Derived datatypes need MPICH's datatype engine,
+ * which is outside this library: MPI_ERR_TYPE. */
 void MPIR_REPLACE(void *invec, void *inoutvec, int *Len, MPI_Datatype * type)
 {
     const MPIR_Type_desc *d = MPIR_Type_lookup(*type);
-    int rc;
-    if (!d) {
-        MPIR_Err_set_detail("MPI_REPLACE: datatype is not a supported basic type");
+    const unsigned h = (unsigned) *type;
+    uint64_t count;
+    int elem, rc;
+    if (d) {
+        elem = d->elem;
+        count = *Len > 0 ? (uint64_t) * Len : 0;
+    } else if ((h >> 30) == 1u && ((h >> 26) & 0xfu) == 0x3u) {         /* builtin-kind datatype */
+        elem = MPIR_HIP_U8;
+        count = *Len > 0 ? (uint64_t) * Len * ((h >> 8) & 0xffu) : 0;
+    } else {
+        MPIR_Err_set_detail("MPI_REPLACE: derived datatypes are not supported by this library");
         op_errno_slot = MPI_ERR_TYPE;
         return;
     }
-    if (*Len <= 0)
+    if (count == 0)
         return;
-    rc = MPIR_Hip_reduce(invec, inoutvec, (uint64_t) * Len, MPIR_HIP_OP_REPLACE, d->elem, NULL, 1);
+    rc = MPIR_Hip_reduce(invec, inoutvec, count, MPIR_HIP_OP_REPLACE, elem, NULL, 1);
     if (rc != MPIR_HIP_OK)
         MPIR_Op_report_hip_error("MPI_REPLACE", rc);
 }

@@ -27,6 +27,9 @@ def _open(path: str) -> ctypes.CDLL:
         f.restype = i32
     lib.oracle_cpu_baseline_sum_f32.argtypes = [i32, ctypes.c_long, i32]
     lib.oracle_cpu_baseline_sum_f32.restype = ctypes.c_double
+    lib.oracle_cpu_baseline_sum_f32_pinned.argtypes = [i32, ctypes.POINTER(i32), ctypes.c_long, i32,
+                                                       ctypes.POINTER(ctypes.c_double)]
+    lib.oracle_cpu_baseline_sum_f32_pinned.restype = ctypes.c_double
     return lib
 
 
@@ -71,3 +74,66 @@ def cpu_baseline_sum_f32(nthreads: int, count: int, iters: int, compiler: str = 
     (compiler "gcc": liboracle.so, MPICH's default build; "clang": liboracle_clang.so)."""
     lib = load_clang() if compiler == "clang" else load()
     return lib.oracle_cpu_baseline_sum_f32(nthreads, count, iters)
+
+
+def physical_cores() -> list[tuple[int, int]]:
+    """(logical cpu, socket) for one logical CPU per physical core among the
+    CPUs this process may run on (sysfs topology: physical_package_id,
+    core_id), lowest sibling first."""
+    try:
+        allowed = sorted(os.sched_getaffinity(0))
+    except AttributeError:
+        allowed = list(range(os.cpu_count() or 1))
+    seen, out = set(), []
+    for c in allowed:
+        base = f"/sys/devices/system/cpu/cpu{c}/topology/"
+        try:
+            pkg = int(open(base + "physical_package_id").read())
+            core = int(open(base + "core_id").read())
+        except (OSError, ValueError):
+            pkg, core = 0, c
+        if (pkg, core) not in seen:
+            seen.add((pkg, core))
+            out.append((c, pkg))
+    return out
+
+
+def cpu_quota() -> float | None:
+    """CPUs' worth of time the cgroup grants this process (cgroup v2 cpu.max or
+    v1 cfs quota / period), None when unlimited or unknown."""
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        return None if q == "max" else int(q) / int(per)
+    except (OSError, ValueError):
+        pass
+    try:
+        q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+        per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+        return None if q <= 0 else q / per
+    except (OSError, ValueError):
+        return None
+
+
+def spread_over_sockets(cores: list[tuple[int, int]], n: int) -> list[tuple[int, int]]:
+    """n of the (cpu, socket) pairs, dealt round-robin over the sockets."""
+    by = {}
+    for c in cores:
+        by.setdefault(c[1], []).append(c)
+    out, k = [], 0
+    while len(out) < min(n, len(cores)):
+        for pkg in sorted(by):
+            if k < len(by[pkg]) and len(out) < n:
+                out.append(by[pkg][k])
+        k += 1
+    return out
+
+
+def cpu_baseline_pinned(cpus: list[int], count: int, iters: int, compiler: str = "gcc") -> list[float]:
+    """One thread pinned per listed CPU, NUMA-local first touch, barrier start;
+    per-thread seconds for `iters` fp32 SUM calls of `count` (negative on failure)."""
+    lib = load_clang() if compiler == "clang" else load()
+    n = len(cpus)
+    arr = (ctypes.c_int * n)(*cpus)
+    secs = (ctypes.c_double * n)()
+    lib.oracle_cpu_baseline_sum_f32_pinned(n, arr, count, iters, secs)
+    return list(secs)
