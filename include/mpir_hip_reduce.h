@@ -96,6 +96,9 @@ int MPIR_Hip_device_count(void);
 /* per-thread contexts (streams, completion word, scratch) created so far; a
    context returns to a pool when its thread exits and is reused, so this stays
    at the peak number of threads calling at once (diagnostic) */
+/* Largest operand (bytes) combined on the calling thread when both operands
+ * are host memory (MPIR_CVAR_REDUCE_LOCAL_HOST_MAX_KB, default 1 MiB). */
+uint64_t MPIR_Hip_host_max_bytes(void);
 int MPIR_Hip_thread_contexts(void);
 
 #ifdef __cplusplus

@@ -276,6 +276,23 @@ CopyPool &copy_pool() {
 
 enum Loc { LOC_HOST = 0, LOC_DEVICE = 1 };
 
+// Both operands in host memory and at most this many bytes each: the combine
+// runs on the calling thread (host_loop, the same functors as the kernels)
+// instead of a staged GPU round trip.  Measured on the MI355X host
+// (tools/host_latency.py, profiles/r02/host_latency_staged.log, host_latency.log), fp32 SUM: a staged
+// call costs 47-50 us up to 16 KiB and 125 us (pinned) / 200 us (pageable) at
+// 1 MiB, the reference's CPU loop 1.8 us at 4 B and 115 us at 1 MiB, 453 us at
+// 4 MiB (GPU: 297 / 505).  MPIR_CVAR_REDUCE_LOCAL_HOST_MAX_KB (default 1024;
+// 0 = always stage through the GPU).
+uint64_t host_max_bytes() {
+    static const uint64_t v = [] {
+        const char *e = getenv("MPIR_CVAR_REDUCE_LOCAL_HOST_MAX_KB");
+        const long kb = e ? atol(e) : 1024;
+        return (uint64_t)(kb >= 0 && kb <= (1L << 22) ? kb : 1024) << 10;
+    }();
+    return v;
+}
+
 // page-locked host memory (hipHostMalloc / hipHostRegister): DMA-able as is
 bool is_pinned_host(const void *p) {
     hipPointerAttribute_t at;
@@ -366,6 +383,8 @@ int MPIR_Hip_has_kernel(int op, int elem) {
 }
 
 const char *MPIR_Hip_error_string(void) { return ctx().err; }
+
+uint64_t MPIR_Hip_host_max_bytes(void) { return host_max_bytes(); }
 
 int MPIR_Hip_thread_contexts(void) {
     std::lock_guard<std::mutex> lk(g_pool_mu);
@@ -478,6 +497,13 @@ int MPIR_Hip_reduce(const void *inbuf, void *inoutbuf, uint64_t count, int op, i
         return rc;
     }
     if (!sync) return MPIR_HIP_EBUFFER;  // the stream variant needs device buffers
+
+    // ---- small, both host-resident: combine on this thread --------------
+    if (lin == LOC_HOST && lio == LOC_HOST && count * esz <= host_max_bytes() && g_table[op][elem].host) {
+        if (MPIR_Hip_device_count() == 0) return MPIR_HIP_ENODEV;
+        g_table[op][elem].host(inbuf, inoutbuf, count * esz / unit);
+        return MPIR_HIP_OK;
+    }
 
     // ---- staged path: at least one operand is host memory (or the two ----
     // ---- operands live on different devices): the up / comp / down      ----

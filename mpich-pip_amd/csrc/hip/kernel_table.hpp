@@ -5,6 +5,9 @@
 //                        32-byte LDS-transpose kernel);
 // g_table[op][elem].any: the one-pass n-operand combine (k_combine_any), the
 //                        general path of MPIR_Hip_combine; REPLACE has none;
+// g_table[op][elem].host: the same combine as a host loop over the same
+//                        functors (reduce_ops.hpp), for small operands that
+//                        both live in host memory (MPIR_Hip_reduce);
 // g_multi[op][elem][order][P = 2, 4, 8]: the fused schedule combines
 //                        (k_combine_multi) for the ops the collectives use most.
 // Storage lives in hip_reduce.hip (zero-initialised); the reg_*.hip units fill
@@ -22,19 +25,38 @@ namespace mpir_hip {
 typedef hipError_t (*launch_fn)(const void *, void *, uint64_t, hipStream_t);
 typedef hipError_t (*any_fn)(const void *const *, int, int, void *, uint64_t, hipStream_t);
 typedef hipError_t (*multi_fn)(const void *const *, void *, uint64_t, hipStream_t);
+typedef void (*host_fn)(const void *, void *, uint64_t);
 
-struct Entry { launch_fn fn; any_fn any; };
+struct Entry { launch_fn fn; any_fn any; host_fn host; };
+
+// inout[i] = Op(inout[i], in[i]) on the host, element by element, through the
+// device functors compiled for x86 (unaligned operands: memcpy'd elements)
+template <class Op, class T>
+void host_loop(const void *in, void *io, uint64_t n) {
+    Op op;
+    const char *pi = static_cast<const char *>(in);
+    char *po = static_cast<char *>(io);
+    for (uint64_t i = 0; i < n; ++i) {
+        T a, b;
+        __builtin_memcpy(&a, po + i * sizeof(T), sizeof(T));
+        __builtin_memcpy(&b, pi + i * sizeof(T), sizeof(T));
+        a = op(a, b);
+        __builtin_memcpy(po + i * sizeof(T), &a, sizeof(T));
+    }
+}
 extern Entry g_table[MPIR_HIP_NOPS][MPIR_HIP_NELEMS];
 extern multi_fn g_multi[MPIR_HIP_NOPS][MPIR_HIP_NELEMS][2][3];
 
 template <class Op, class T>
 void reg(int op, int elem) {
     g_table[op][elem].fn = &launch_reduce<Op, T>;
+    g_table[op][elem].host = &host_loop<Op, T>;
     if constexpr (!__is_same(Op, OpReplace)) g_table[op][elem].any = &launch_combine_any<Op, T>;
 }
 template <class Op, class T, int EPL = 2>
 void reg_wide(int op, int elem) {
     g_table[op][elem].fn = &launch_reduce_wide<Op, T, EPL>;
+    g_table[op][elem].host = &host_loop<Op, T>;
     g_table[op][elem].any = &launch_combine_any<Op, T>;
 }
 template <class Op, class T>

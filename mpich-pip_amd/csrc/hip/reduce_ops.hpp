@@ -27,6 +27,11 @@
 #include <stdint.h>
 #include "x87.hpp"
 
+// Every functor is host + device: the GPU kernels and the host combine for
+// small host-resident operands (hip_reduce.hip, host_loop below) share one
+// definition of each op's semantics.
+#define MPIR_HD __host__ __device__ __forceinline__
+
 namespace mpir_hip {
 
 typedef _Float16 f16;
@@ -44,7 +49,7 @@ struct pldint    { x80 value; int32_t loc; int32_t pad_[3]; };       // 32 B (MP
 struct cx80      { x80 re, im; };                                     // 32 B (long double _Complex)
 
 // b's value stored into a's slot: fstpt writes 10 bytes, a's padding stays
-__device__ __forceinline__ x80 x80_into(const x80 &b, const x80 &a) {
+MPIR_HD x80 x80_into(const x80 &b, const x80 &a) {
     x80 r = a;
     r.m = b.m;
     r.se = b.se;
@@ -81,42 +86,42 @@ template <> struct FP<_Float16> {
     static constexpr U quiet = 0x0200u, indefinite = 0xfe00u;
 };
 
-template <class R> __device__ __forceinline__ bool isnan_(R x) { return x != x; }
-template <class R> __device__ __forceinline__ R quiet_(R x) {
+template <class R> MPIR_HD bool isnan_(R x) { return x != x; }
+template <class R> MPIR_HD R quiet_(R x) {
     typedef typename FP<R>::U U;
     return __builtin_bit_cast(R, (U)(__builtin_bit_cast(U, x) | FP<R>::quiet));
 }
-template <class R> __device__ __forceinline__ R x86_result(R p, R q, R r) {
+template <class R> MPIR_HD R x86_result(R p, R q, R r) {
     typedef typename FP<R>::U U;
     if (isnan_(p)) return quiet_(p);
     if (isnan_(q)) return quiet_(q);
     if (isnan_(r)) return __builtin_bit_cast(R, (U)FP<R>::indefinite);
     return r;
 }
-template <class R> __device__ __forceinline__ R xadd(R p, R q) { return x86_result(p, q, (R)(p + q)); }
-template <class R> __device__ __forceinline__ R xsub(R p, R q) { return x86_result(p, q, (R)(p - q)); }
-template <class R> __device__ __forceinline__ R xmul(R p, R q) { return x86_result(p, q, (R)(p * q)); }
+template <class R> MPIR_HD R xadd(R p, R q) { return x86_result(p, q, (R)(p + q)); }
+template <class R> MPIR_HD R xsub(R p, R q) { return x86_result(p, q, (R)(p - q)); }
+template <class R> MPIR_HD R xmul(R p, R q) { return x86_result(p, q, (R)(p * q)); }
 
 // ---------------------------------------------------------------- arithmetic
 struct OpSum {
-    template <class T> __device__ __forceinline__ T operator()(T a, T b) const {
+    template <class T> MPIR_HD T operator()(T a, T b) const {
         typedef typename uns<T>::type U;
         return (T)(U)((U)a + (U)b);
     }
-    __device__ __forceinline__ f16 operator()(f16 a, f16 b) const { return xadd(a, b); }
-    __device__ __forceinline__ float operator()(float a, float b) const { return xadd(a, b); }
-    __device__ __forceinline__ double operator()(double a, double b) const { return xadd(a, b); }
-    __device__ __forceinline__ cf32 operator()(cf32 a, cf32 b) const { return cf32{xadd(a.re, b.re), xadd(a.im, b.im)}; }
-    __device__ __forceinline__ cf64 operator()(cf64 a, cf64 b) const { return cf64{xadd(a.re, b.re), xadd(a.im, b.im)}; }
-    __device__ __forceinline__ x80 operator()(x80 a, x80 b) const { return x80_add(a, b, a); }
-    __device__ __forceinline__ cx80 operator()(cx80 a, cx80 b) const {
+    MPIR_HD f16 operator()(f16 a, f16 b) const { return xadd(a, b); }
+    MPIR_HD float operator()(float a, float b) const { return xadd(a, b); }
+    MPIR_HD double operator()(double a, double b) const { return xadd(a, b); }
+    MPIR_HD cf32 operator()(cf32 a, cf32 b) const { return cf32{xadd(a.re, b.re), xadd(a.im, b.im)}; }
+    MPIR_HD cf64 operator()(cf64 a, cf64 b) const { return cf64{xadd(a.re, b.re), xadd(a.im, b.im)}; }
+    MPIR_HD x80 operator()(x80 a, x80 b) const { return x80_add(a, b, a); }
+    MPIR_HD cx80 operator()(cx80 a, cx80 b) const {
         return cx80{x80_add(a.re, b.re, a.re), x80_add(a.im, b.im, a.im)};
     }
     // fast path for real types: a NaN operand or an invalid operation always
     // yields a NaN result, so the x86 rule only needs to run when the plain
     // result is NaN (see combine16 / fold_elems)
     static constexpr bool kNanFast = true;
-    template <class R> static __device__ __forceinline__ R raw(R a, R b) { return a + b; }
+    template <class R> static MPIR_HD R raw(R a, R b) { return a + b; }
 };
 
 // C99 Annex G complex multiply (a + ib) * (c + id), as gcc emits it for
@@ -124,7 +129,7 @@ struct OpSum {
 // ad = a*d, y = ad + bc, left operand first), then the __mulsc3/__muldc3
 // recovery when both parts come out NaN.
 template <class R>
-__device__ __forceinline__ void annexg_mul(R a, R b, R c, R d, R &x, R &y) {
+MPIR_HD void annexg_mul(R a, R b, R c, R d, R &x, R &y) {
     R ac = xmul(a, c), bd = xmul(b, d), ad = xmul(a, d), bc = xmul(b, c);
     x = xsub(ac, bd);
     y = xadd(ad, bc);
@@ -160,25 +165,25 @@ __device__ __forceinline__ void annexg_mul(R a, R b, R c, R d, R &x, R &y) {
 }
 
 struct OpProd {
-    template <class T> __device__ __forceinline__ T operator()(T a, T b) const {
+    template <class T> MPIR_HD T operator()(T a, T b) const {
         typedef typename uns<T>::type U;
         return (T)(U)((U)a * (U)b);
     }
-    __device__ __forceinline__ f16 operator()(f16 a, f16 b) const { return xmul(a, b); }
-    __device__ __forceinline__ float operator()(float a, float b) const { return xmul(a, b); }
-    __device__ __forceinline__ double operator()(double a, double b) const { return xmul(a, b); }
-    __device__ __forceinline__ cf32 operator()(cf32 a, cf32 b) const {
+    MPIR_HD f16 operator()(f16 a, f16 b) const { return xmul(a, b); }
+    MPIR_HD float operator()(float a, float b) const { return xmul(a, b); }
+    MPIR_HD double operator()(double a, double b) const { return xmul(a, b); }
+    MPIR_HD cf32 operator()(cf32 a, cf32 b) const {
         cf32 r; annexg_mul<float>(a.re, a.im, b.re, b.im, r.re, r.im); return r;
     }
-    __device__ __forceinline__ cf64 operator()(cf64 a, cf64 b) const {
+    MPIR_HD cf64 operator()(cf64 a, cf64 b) const {
         cf64 r; annexg_mul<double>(a.re, a.im, b.re, b.im, r.re, r.im); return r;
     }
-    __device__ __forceinline__ x80 operator()(x80 a, x80 b) const { return x80_mul(a, b, a); }
-    __device__ __forceinline__ cx80 operator()(cx80 a, cx80 b) const {
+    MPIR_HD x80 operator()(x80 a, x80 b) const { return x80_mul(a, b, a); }
+    MPIR_HD cx80 operator()(cx80 a, cx80 b) const {
         cx80 r; x80_cmul(a.re, a.im, b.re, b.im, r.re, r.im); return r;
     }
     static constexpr bool kNanFast = true;
-    template <class R> static __device__ __forceinline__ R raw(R a, R b) { return a * b; }
+    template <class R> static MPIR_HD R raw(R a, R b) { return a * b; }
 };
 
 template <class Op, class = void> struct has_nan_fast { static constexpr bool value = false; };
@@ -196,48 +201,48 @@ template <class Op, class T> struct nan_fast {
 
 // MPL_MAX(a,b) (((a) > (b)) ? (a) : (b)); a = inout, b = in
 struct OpMax {
-    template <class T> __device__ __forceinline__ T operator()(T a, T b) const { return (a > b) ? a : b; }
-    __device__ __forceinline__ x80 operator()(x80 a, x80 b) const { return x80_gt(a, b) ? a : x80_into(b, a); }
+    template <class T> MPIR_HD T operator()(T a, T b) const { return (a > b) ? a : b; }
+    MPIR_HD x80 operator()(x80 a, x80 b) const { return x80_gt(a, b) ? a : x80_into(b, a); }
 };
 struct OpMin {
-    template <class T> __device__ __forceinline__ T operator()(T a, T b) const { return (a < b) ? a : b; }
-    __device__ __forceinline__ x80 operator()(x80 a, x80 b) const { return x80_lt(a, b) ? a : x80_into(b, a); }
+    template <class T> MPIR_HD T operator()(T a, T b) const { return (a < b) ? a : b; }
+    MPIR_HD x80 operator()(x80 a, x80 b) const { return x80_lt(a, b) ? a : x80_into(b, a); }
 };
 
 // ---------------------------------------------------------------- logical
-template <class T> __device__ __forceinline__ bool truth(T v) { return v != (T)0; }
+template <class T> MPIR_HD bool truth(T v) { return v != (T)0; }
 
 struct OpLand {
-    template <class T> __device__ __forceinline__ T operator()(T a, T b) const { return (T)(truth(a) && truth(b)); }
+    template <class T> MPIR_HD T operator()(T a, T b) const { return (T)(truth(a) && truth(b)); }
 };
 struct OpLor {
-    template <class T> __device__ __forceinline__ T operator()(T a, T b) const { return (T)(truth(a) || truth(b)); }
+    template <class T> MPIR_HD T operator()(T a, T b) const { return (T)(truth(a) || truth(b)); }
 };
 struct OpLxor {
-    template <class T> __device__ __forceinline__ T operator()(T a, T b) const {
+    template <class T> MPIR_HD T operator()(T a, T b) const {
         return (T)((truth(a) && !truth(b)) || (!truth(a) && truth(b)));
     }
     // the 0/1 int result is converted (fildl) and stored with fstpt
-    __device__ __forceinline__ x80 operator()(x80 a, x80 b) const {
+    MPIR_HD x80 operator()(x80 a, x80 b) const {
         return (x80_truth(a) != x80_truth(b)) ? x80_one(a) : x80_zero(a);
     }
 };
 
 // ---------------------------------------------------------------- bitwise
-struct OpBand { template <class T> __device__ __forceinline__ T operator()(T a, T b) const { return (T)(a & b); } };
-struct OpBor  { template <class T> __device__ __forceinline__ T operator()(T a, T b) const { return (T)(a | b); } };
-struct OpBxor { template <class T> __device__ __forceinline__ T operator()(T a, T b) const { return (T)(a ^ b); } };
+struct OpBand { template <class T> MPIR_HD T operator()(T a, T b) const { return (T)(a & b); } };
+struct OpBor  { template <class T> MPIR_HD T operator()(T a, T b) const { return (T)(a | b); } };
+struct OpBxor { template <class T> MPIR_HD T operator()(T a, T b) const { return (T)(a ^ b); } };
 
 // ---------------------------------------------------------------- loc pairs
 // opmaxloc.c:48-59: if (a.value < b.value) a = b;
 //                   else if (a.value <= b.value) a.loc = MPL_MIN(a.loc, b.loc);
 struct OpMaxloc {
-    template <class P> __device__ __forceinline__ P operator()(P a, P b) const {
+    template <class P> MPIR_HD P operator()(P a, P b) const {
         if (a.value < b.value) { a.value = b.value; a.loc = b.loc; }
         else if (a.value <= b.value) a.loc = (a.loc < b.loc) ? a.loc : b.loc;
         return a;
     }
-    __device__ __forceinline__ pldint operator()(pldint a, pldint b) const {
+    MPIR_HD pldint operator()(pldint a, pldint b) const {
         if (x80_lt(a.value, b.value)) { a.value = x80_into(b.value, a.value); a.loc = b.loc; }
         else if (x80_le(a.value, b.value)) a.loc = (a.loc < b.loc) ? a.loc : b.loc;
         return a;
@@ -245,12 +250,12 @@ struct OpMaxloc {
 };
 // opminloc.c:48-59 (mirror with > / >=)
 struct OpMinloc {
-    template <class P> __device__ __forceinline__ P operator()(P a, P b) const {
+    template <class P> MPIR_HD P operator()(P a, P b) const {
         if (a.value > b.value) { a.value = b.value; a.loc = b.loc; }
         else if (a.value >= b.value) a.loc = (a.loc < b.loc) ? a.loc : b.loc;
         return a;
     }
-    __device__ __forceinline__ pldint operator()(pldint a, pldint b) const {
+    MPIR_HD pldint operator()(pldint a, pldint b) const {
         if (x80_gt(a.value, b.value)) { a.value = x80_into(b.value, a.value); a.loc = b.loc; }
         else if (x80_ge(a.value, b.value)) a.loc = (a.loc < b.loc) ? a.loc : b.loc;
         return a;
@@ -259,7 +264,7 @@ struct OpMinloc {
 
 // REPLACE (opreplace.c:15 -> MPIR_Localcopy): inout = in
 struct OpReplace {
-    template <class T> __device__ __forceinline__ T operator()(T, T b) const { return b; }
+    template <class T> MPIR_HD T operator()(T, T b) const { return b; }
 };
 
 }  // namespace mpir_hip

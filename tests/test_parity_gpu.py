@@ -618,3 +618,45 @@ def test_replace_every_predefined_type(mpi, cuda, dtname, handle, size):
     ty2 = ctypes.c_int(0x8c000100)
     lib.MPIR_REPLACE(ctypes.c_void_p(pin), ctypes.c_void_p(pio), ctypes.byref(ln), ctypes.byref(ty2))
     assert errno_slot()[0] == mpi.MPI_ERR_TYPE
+
+
+def run_pair_host(mpi, orc, op, t, n, seed, off=0):
+    """Both operands in pageable host memory (byte offset `off`): at most
+    MPIR_Hip_host_max_bytes() per operand the combine runs on the calling
+    thread through the same functors as the kernels (hip_reduce.hip)."""
+    rng = np.random.default_rng(seed)
+    a = T.to_bytes(T.gen(t, n, rng, op))
+    b = T.to_bytes(T.gen(t, n, rng, op))
+    want = a.copy()
+    rc_o = orc.reduce_local(b.copy(), want, n, mpi.DATATYPES[t], mpi.OPS[op])
+    ha = np.zeros(a.size + off, np.uint8)
+    hb = np.zeros(b.size + off, np.uint8)
+    ha[off:] = a
+    hb[off:] = b
+    rc = mpi.reduce_local(hb.ctypes.data + off, ha.ctypes.data + off, n, mpi.DATATYPES[t], mpi.OPS[op])
+    got = ha[off:]
+    assert mpi.error_class(rc) == rc_o, (op, t, rc, rc_o)
+    assert np.array_equal(hb[off:], b), "inbuf modified"
+    if not same(got, want, t):
+        pytest.fail(f"host {op} {t} n={n} off={off}:\n" + explain(got, want, a, b, T.elem_size(t)))
+
+
+@pytest.mark.parametrize("op,t", MATRIX, ids=[f"{o}-{t}" for o, t in MATRIX])
+def test_host_path_matrix_vs_oracle(mpi, orc, cuda, op, t):
+    """Small host-resident operands (the host combine), every (op, type) pair,
+    edge values included, aligned and misaligned."""
+    for n, seed, off in ((1, 11, 0), (7, 12, 3), (1000, 13, 0), (4099, 14, 1)):
+        run_pair_host(mpi, orc, op, t, n, seed, off)
+
+
+def test_host_path_crossover(mpi, orc, cuda):
+    """Either side of MPIR_Hip_host_max_bytes (host combine below, GPU staging
+    above): both bit-exact, for a float and a complex and a pair type."""
+    lib = mpi.load()
+    lib.MPIR_Hip_host_max_bytes.restype = ctypes.c_uint64
+    lim = lib.MPIR_Hip_host_max_bytes()
+    assert lim == 1 << 20
+    for op, t in (("MPI_SUM", "MPI_FLOAT"), ("MPI_PROD", "MPI_C_DOUBLE_COMPLEX"), ("MPI_MAXLOC", "MPI_DOUBLE_INT")):
+        esz = T.elem_size(t)
+        for n in (lim // esz, lim // esz + 1):
+            run_pair_host(mpi, orc, op, t, n, 21 + n)

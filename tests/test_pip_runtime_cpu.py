@@ -95,7 +95,7 @@ def test_builtin_reduce_without_gpu_fails_loudly(prog, mpi):
     cpi = os.path.join(ROOT, "examples", "cpi")
     r = run(2, cpi)
     assert r.returncode == 1
-    assert "Fatal error in MPI_Reduce" in r.stderr and "no ROCm-capable device" in r.stderr
+    assert "Fatal error in MPI_Reduce" in r.stderr and "no HIP device available" in r.stderr
     assert "pi is approximately" not in r.stdout
 
 
