@@ -192,9 +192,36 @@ def main():
     ok_sc = bool(np.array_equal(srecv.cpu().numpy().view(np.uint32), expect_scan(xs, rank).view(np.uint32)))
     ex = expect_scan(xs, rank, exclusive=True)
     ok_ex = True if ex is None else bool(np.array_equal(erecv.cpu().numpy().view(np.uint32), ex.view(np.uint32)))
-    flags = torch.tensor([float(ok_ar), float(ok_rs), float(ok_rd), float(ok_sc), float(ok_ex)],
-                         dtype=torch.float64, device="cuda")
-    assert m.allreduce(m.MPI_IN_PLACE, flags.data_ptr(), 5, m.MPI_DOUBLE, m.MPI_MIN, C, RCCL) == 0
+    # RCCL mode (tests/test_coll_rccl_gpu.py's checks at this world size): RCCL
+    # reorders the sum, so fp32/fp16 against the reference association within
+    # |got - ref| <= gamma_{p-1} * sum|x_i|; int32 exact
+    rrecv = torch.zeros_like(send)
+    torch.cuda.synchronize()
+    assert m.allreduce(send.data_ptr(), rrecv.data_ptr(), n, F32, SUM, C, RCCL) == 0
+    ref64 = expect_allreduce(xs).astype(np.float64) if pof2 else np.sum([x.astype(np.float64) for x in xs], axis=0)
+    mag = np.sum([np.abs(x.astype(np.float64)) for x in xs], axis=0)
+    g32 = (world - 1) * 2.0 ** -24 / (1 - (world - 1) * 2.0 ** -24)
+    ok_rccl_ar = bool(np.all(np.abs(rrecv.cpu().numpy().astype(np.float64) - ref64) <= g32 * mag + 1e-45))
+    hr2 = torch.zeros(rcount, dtype=torch.float16, device="cuda")
+    torch.cuda.synchronize()
+    assert m.reduce_scatter_block(hsend.data_ptr(), hr2.data_ptr(), rcount, F16, SUM, C, RCCL) == 0
+    sl = slice(rank * rcount, (rank + 1) * rcount)
+    href = expect_reduce_scatter_block(hs, rank, rcount).astype(np.float64)
+    hmag = np.sum([np.abs(h[sl].astype(np.float64)) for h in hs], axis=0)
+    g16 = (world - 1) * 2.0 ** -11 / (1 - (world - 1) * 2.0 ** -11)
+    # the reference chain rounds to fp16 at every step too: allow both chains' error
+    ok_rccl_rs = bool(np.all(np.abs(hr2.cpu().numpy().astype(np.float64) - href) <= 2 * g16 * hmag + 2.0 ** -24))
+    ints = [np.random.default_rng(300 + r).integers(-2 ** 31, 2 ** 31, 4099, dtype=np.int64).astype(np.int32)
+            for r in range(world)]
+    isend = torch.from_numpy(ints[rank].copy()).cuda()
+    irecv = torch.zeros_like(isend)
+    torch.cuda.synchronize()
+    assert m.allreduce(isend.data_ptr(), irecv.data_ptr(), 4099, m.MPI_INT, SUM, C, RCCL) == 0
+    iwant = np.sum([x.astype(np.int64) for x in ints], axis=0).astype(np.uint32).view(np.int32)
+    ok_rccl_int = bool(np.array_equal(irecv.cpu().numpy(), iwant))
+    flags = torch.tensor([float(ok_ar), float(ok_rs), float(ok_rd), float(ok_sc), float(ok_ex), float(ok_rccl_ar),
+                          float(ok_rccl_rs), float(ok_rccl_int)], dtype=torch.float64, device="cuda")
+    assert m.allreduce(m.MPI_IN_PLACE, flags.data_ptr(), 8, m.MPI_DOUBLE, m.MPI_MIN, C, RCCL) == 0
     out["parity_reference_order"] = {
         "allreduce_fp32_sum_bitexact": bool(flags[0].item() == 1.0) if pof2 else "not checked (non-pof2 N)",
         "reduce_scatter_block_fp16_sum_bitexact": bool(flags[1].item() == 1.0),
@@ -202,6 +229,11 @@ def main():
         "scan_fp32_sum_bitexact": bool(flags[3].item() == 1.0),
         "exscan_fp32_sum_bitexact": bool(flags[4].item() == 1.0),
         "checker": "numpy, same association (full oracle parity: tests/test_coll_*)"}
+    out["parity_rccl"] = {
+        "allreduce_fp32_sum_within_gamma": bool(flags[5].item() == 1.0),
+        "reduce_scatter_block_fp16_sum_within_gamma": bool(flags[6].item() == 1.0),
+        "allreduce_int32_sum_exact": bool(flags[7].item() == 1.0),
+        "tolerance": "|got - ref| <= gamma_{p-1} * sum|x_i|, gamma_k = k u / (1 - k u) (SURVEY.md §8c)"}
 
     # ---- 2. timing
     def timed(fn):
