@@ -99,6 +99,11 @@ int MPIR_Hip_device_count(void);
 /* Largest operand (bytes) combined on the calling thread when both operands
  * are host memory (MPIR_CVAR_REDUCE_LOCAL_HOST_MAX_KB, default 1 MiB). */
 uint64_t MPIR_Hip_host_max_bytes(void);
+
+/* Synchronous device-resident reductions completed through the direct AQL
+ * dispatch (direct_dispatch.hip) so far in this process (0 with
+ * MPIR_CVAR_REDUCE_LOCAL_DISPATCH=hip or where the path is unavailable). */
+uint64_t MPIR_Hip_direct_dispatches(void);
 int MPIR_Hip_thread_contexts(void);
 
 #ifdef __cplusplus

@@ -1,0 +1,342 @@
+// direct_dispatch.hip -- synchronous device-resident MPI_Reduce_local without
+// the HIP launch path: our own AQL queue, the tile kernel from a device-only
+// code object (direct_tiles.hip -> lib/libmpir_hip_tiles.hsaco), kernargs in
+// VRAM, and a wait on the dispatch packet's own completion signal.
+//
+// Why (tools/aql/aql2.cpp, profiles/r02/aql2_*.log): a synchronous HIP call
+// is hipLaunchKernel + a completion word written by hipStreamWriteValue32,
+// which is a second (blit) dispatch; the GPU then sits idle 8.8-8.9 us between
+// one call's last workgroup and the next call's first.  A direct dispatch
+// waits on the kernel packet's completion signal instead: 7.4-7.5 us, and the
+// 256 MiB fp32 SUM call 126.2-126.4 us against 127.6-127.8 (same box, same
+// kernel).  An earlier attempt (round 1) lost because its kernargs sat in host
+// memory (every workgroup read them over PCIe); here they are written through
+// the BAR into VRAM and made visible with an HDP flush (the register ROCr
+// exposes as HSA_AMD_AGENT_INFO_HDP_FLUSH; read back, as HIP does for its
+// device kernargs), before the packet header is published.
+//
+// Scope and ordering (the HIP path is used whenever one does not hold):
+//   * synchronous calls on the library's own stream (hip_stream NULL), both
+//     operands on one device, 16 B-aligned with no head / tail elements (the
+//     lean tile kernel), an (op, element) pair the code object carries;
+//   * the legacy null stream is idle (hipStreamQuery(NULL) == hipSuccess, 0.11
+//     us): work the caller queued there for these buffers stays ordered before
+//     the reduction, as with the blocking HIP stream;
+//   * the calling thread has no unfinished work on its own library stream.
+// Packets carry an agent-scope acquire (what HIP uses between kernels; a
+// system-scope acquire costs ~7 us of body, aql_sig_nt_sys) and a
+// system-scope release, so the result is visible to every agent -- SDMA
+// copies and the host included -- when the signal fires.  One queue per
+// device, shared by the threads; a mutex orders packet publication (single
+// producer at a time, doorbell monotonic); no barrier bit, so concurrent
+// threads' kernels overlap; each thread waits on its own signal.
+// MPIR_CVAR_REDUCE_LOCAL_DISPATCH=hip turns the path off.
+#include <hip/hip_runtime.h>
+#include <hsa/hsa.h>
+#include <hsa/hsa_ext_amd.h>
+#include <dlfcn.h>
+#include <immintrin.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <atomic>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "mpir_hip_reduce.h"
+#include "kernel_table.hpp"
+
+namespace mpir_hip {
+
+namespace {
+
+constexpr int kMaxDirectDev = 64;
+constexpr uint32_t kKargSlots = 256, kKargSlotBytes = 64;
+constexpr uint32_t kQueueSize = 256;
+
+struct KArgs {          // the tile kernel's four explicit arguments (32 bytes)
+    const char *in;
+    char *io;
+    uint64_t vbytes;
+    uint64_t keep;
+};
+
+struct DevState {
+    std::once_flag once;
+    bool ok = false;
+    hsa_agent_t agent{};
+    hsa_queue_t *queue = nullptr;
+    char *karg = nullptr;                       // kKargSlots x kKargSlotBytes, VRAM, host-written
+    std::atomic<uint32_t> kslot{0};
+    volatile uint32_t *hdp = nullptr;
+    uint64_t kobj[MPIR_HIP_NOPS][MPIR_HIP_NELEMS] = {};
+    std::mutex publish;
+    std::atomic<int> queue_error{0};
+};
+
+DevState g_dev[kMaxDirectDev];
+std::atomic<uint64_t> g_direct_calls{0};
+
+int mode() {
+    static const int m = [] {
+        const char *e = getenv("MPIR_CVAR_REDUCE_LOCAL_DISPATCH");
+        return (e && !strcmp(e, "hip")) ? 0 : 1;
+    }();
+    return m;
+}
+
+struct Find {
+    uint32_t bdf, domain;
+    hsa_agent_t gpu{}, cpu{};
+    bool have_gpu = false, have_cpu = false;
+    hsa_amd_memory_pool_t vram{};
+    bool have_vram = false;
+};
+
+hsa_status_t find_agent(hsa_agent_t a, void *p) {
+    Find *f = static_cast<Find *>(p);
+    hsa_device_type_t t;
+    if (hsa_agent_get_info(a, HSA_AGENT_INFO_DEVICE, &t) != HSA_STATUS_SUCCESS) return HSA_STATUS_SUCCESS;
+    if (t == HSA_DEVICE_TYPE_CPU && !f->have_cpu) {
+        f->cpu = a;
+        f->have_cpu = true;
+    } else if (t == HSA_DEVICE_TYPE_GPU) {
+        uint32_t bdf = 0, dom = 0;
+        hsa_agent_get_info(a, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_BDFID, &bdf);
+        hsa_agent_get_info(a, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_DOMAIN, &dom);
+        if (bdf == f->bdf && dom == f->domain) {
+            f->gpu = a;
+            f->have_gpu = true;
+        }
+    }
+    return HSA_STATUS_SUCCESS;
+}
+
+hsa_status_t find_vram(hsa_amd_memory_pool_t p, void *arg) {
+    Find *f = static_cast<Find *>(arg);
+    hsa_amd_segment_t seg;
+    uint32_t flags = 0;
+    hsa_amd_memory_pool_get_info(p, HSA_AMD_MEMORY_POOL_INFO_SEGMENT, &seg);
+    if (seg != HSA_AMD_SEGMENT_GLOBAL) return HSA_STATUS_SUCCESS;
+    hsa_amd_memory_pool_get_info(p, HSA_AMD_MEMORY_POOL_INFO_GLOBAL_FLAGS, &flags);
+    if (flags & HSA_AMD_MEMORY_POOL_GLOBAL_FLAG_COARSE_GRAINED) {
+        f->vram = p;
+        f->have_vram = true;
+        return HSA_STATUS_INFO_BREAK;
+    }
+    return HSA_STATUS_SUCCESS;
+}
+
+void queue_error_cb(hsa_status_t status, hsa_queue_t *q, void *data) {
+    (void)q;
+    DevState *d = static_cast<DevState *>(data);
+    d->queue_error.store((int)status ? (int)status : -1);
+    const char *msg = nullptr;
+    hsa_status_string(status, &msg);
+    fprintf(stderr, "mpir_hip: direct-dispatch queue error: %s\n", msg ? msg : "?");
+}
+
+// the code object sits next to this library
+std::string tiles_path() {
+    Dl_info info;
+    if (!dladdr((void *)&tiles_path, &info) || !info.dli_fname) return "";
+    std::string p = info.dli_fname;
+    const size_t slash = p.rfind('/');
+    p = (slash == std::string::npos ? std::string(".") : p.substr(0, slash)) + "/libmpir_hip_tiles.hsaco";
+    return p;
+}
+
+const char *op_name(int op) {
+    switch (op) {
+    case MPIR_HIP_OP_SUM: return "SUM";
+    case MPIR_HIP_OP_PROD: return "PROD";
+    case MPIR_HIP_OP_MAX: return "MAX";
+    case MPIR_HIP_OP_MIN: return "MIN";
+    default: return nullptr;
+    }
+}
+
+const char *elem_name(int e) {
+#define N(E) case E: return #E;
+    switch (e) {
+        N(MPIR_HIP_I8) N(MPIR_HIP_U8) N(MPIR_HIP_I16) N(MPIR_HIP_U16) N(MPIR_HIP_I32) N(MPIR_HIP_U32)
+        N(MPIR_HIP_I64) N(MPIR_HIP_U64) N(MPIR_HIP_F16) N(MPIR_HIP_F32) N(MPIR_HIP_F64) N(MPIR_HIP_CF32)
+        N(MPIR_HIP_CF64)
+    default: return nullptr;
+    }
+#undef N
+}
+
+void init_dev(int dev, DevState &d) {
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, dev) != hipSuccess) { (void)hipGetLastError(); return; }
+    Find f;
+    f.bdf = ((uint32_t)prop.pciBusID << 8) | ((uint32_t)prop.pciDeviceID << 3);
+    f.domain = (uint32_t)prop.pciDomainID;
+    if (hsa_init() != HSA_STATUS_SUCCESS) return;
+    hsa_iterate_agents(find_agent, &f);
+    if (!f.have_gpu || !f.have_cpu) return;
+    hsa_amd_agent_iterate_memory_pools(f.gpu, find_vram, &f);
+    if (!f.have_vram) return;
+    hsa_amd_hdp_flush_t hdp{};
+    if (hsa_agent_get_info(f.gpu, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_HDP_FLUSH, &hdp) != HSA_STATUS_SUCCESS ||
+        !hdp.HDP_MEM_FLUSH_CNTL)
+        return;
+    // code object
+    const std::string path = tiles_path();
+    FILE *fp = path.empty() ? nullptr : fopen(path.c_str(), "rb");
+    if (!fp) return;
+    std::vector<char> co;
+    char buf[65536];
+    size_t n;
+    while ((n = fread(buf, 1, sizeof buf, fp)) > 0) co.insert(co.end(), buf, buf + n);
+    fclose(fp);
+    hsa_code_object_reader_t rd;
+    hsa_executable_t exe;
+    if (hsa_code_object_reader_create_from_memory(co.data(), co.size(), &rd) != HSA_STATUS_SUCCESS) return;
+    if (hsa_executable_create_alt(HSA_PROFILE_FULL, HSA_DEFAULT_FLOAT_ROUNDING_MODE_DEFAULT, nullptr, &exe) !=
+            HSA_STATUS_SUCCESS ||
+        hsa_executable_load_agent_code_object(exe, f.gpu, rd, nullptr, nullptr) != HSA_STATUS_SUCCESS ||
+        hsa_executable_freeze(exe, nullptr) != HSA_STATUS_SUCCESS)
+        return;     // (the reader and executable live as long as the process)
+    int found = 0;
+    for (int op = 1; op < MPIR_HIP_NOPS; ++op) {
+        for (int e = 1; e < MPIR_HIP_NELEMS; ++e) {
+            if (!op_name(op) || !elem_name(e)) continue;
+            const std::string sym = std::string("mpir_tile_") + op_name(op) + "_" + elem_name(e) + ".kd";
+            hsa_executable_symbol_t s;
+            uint64_t ko = 0;
+            uint32_t kas = 0;
+            if (hsa_executable_get_symbol_by_name(exe, sym.c_str(), &f.gpu, &s) != HSA_STATUS_SUCCESS) continue;
+            if (hsa_executable_symbol_get_info(s, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_OBJECT, &ko) != HSA_STATUS_SUCCESS ||
+                hsa_executable_symbol_get_info(s, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_KERNARG_SEGMENT_SIZE, &kas) !=
+                    HSA_STATUS_SUCCESS ||
+                kas != sizeof(KArgs))
+                continue;
+            d.kobj[op][e] = ko;
+            ++found;
+        }
+    }
+    if (!found) return;
+    // kernargs in VRAM, host-writable
+    void *kp = nullptr;
+    if (hsa_amd_memory_pool_allocate(f.vram, (size_t)kKargSlots * kKargSlotBytes, 0, &kp) != HSA_STATUS_SUCCESS) return;
+    if (hsa_amd_agents_allow_access(1, &f.cpu, nullptr, kp) != HSA_STATUS_SUCCESS) {
+        hsa_amd_memory_pool_free(kp);
+        return;
+    }
+    if (hsa_queue_create(f.gpu, kQueueSize, HSA_QUEUE_TYPE_MULTI, queue_error_cb, &d, UINT32_MAX, UINT32_MAX,
+                         &d.queue) != HSA_STATUS_SUCCESS) {
+        hsa_amd_memory_pool_free(kp);
+        return;
+    }
+    d.agent = f.gpu;
+    d.karg = static_cast<char *>(kp);
+    d.hdp = hdp.HDP_MEM_FLUSH_CNTL;
+    d.ok = true;
+}
+
+}  // namespace
+
+// Completion signals, one per (thread, device).  A thread's signals go back
+// to a process-wide free list when it exits (no HSA call at thread exit) and
+// the next new thread takes them, so threads that come and go reuse a bounded
+// set.
+std::mutex g_sig_mu;
+std::vector<hsa_signal_t> g_sig_free[kMaxDirectDev];
+
+struct DirectSignals {
+    hsa_signal_t sig[kMaxDirectDev] = {};
+    bool have[kMaxDirectDev] = {};
+    bool get(int dev, hsa_signal_t *out) {
+        if (!have[dev]) {
+            {
+                std::lock_guard<std::mutex> lk(g_sig_mu);
+                if (!g_sig_free[dev].empty()) {
+                    sig[dev] = g_sig_free[dev].back();
+                    g_sig_free[dev].pop_back();
+                    have[dev] = true;
+                }
+            }
+            if (!have[dev]) {
+                if (hsa_signal_create(0, 0, nullptr, &sig[dev]) != HSA_STATUS_SUCCESS) return false;
+                have[dev] = true;
+            }
+        }
+        *out = sig[dev];
+        return true;
+    }
+    ~DirectSignals() {
+        std::lock_guard<std::mutex> lk(g_sig_mu);
+        for (int i = 0; i < kMaxDirectDev; ++i)
+            if (have[i]) g_sig_free[i].push_back(sig[i]);
+    }
+};
+thread_local DirectSignals t_sig;
+
+// 1: dispatched and completed (rc set); 0: not applicable, use the HIP path
+int direct_reduce(int dev, int op, int elem, const void *in, void *io, uint64_t vbytes, int *rc) {
+    if (mode() == 0 || dev < 0 || dev >= kMaxDirectDev || op <= 0 || op >= MPIR_HIP_NOPS || elem <= 0 ||
+        elem >= MPIR_HIP_NELEMS)
+        return 0;
+    DevState &d = g_dev[dev];
+    std::call_once(d.once, [&] { init_dev(dev, d); });
+    if (!d.ok || d.queue_error.load(std::memory_order_relaxed)) return 0;
+    const uint64_t ko = d.kobj[op][elem];
+    if (!ko || vbytes == 0 || vbytes / 16384 >= (1ull << 26)) return 0;
+    // work queued on the legacy null stream stays ordered before us
+    if (hipStreamQuery(nullptr) != hipSuccess) {
+        (void)hipGetLastError();
+        return 0;
+    }
+    hsa_signal_t sig;
+    if (!t_sig.get(dev, &sig)) return 0;
+    const uint32_t groups = (uint32_t)((vbytes + kTileBytes - 1) / kTileBytes);
+    const KArgs ka{static_cast<const char *>(in), static_cast<char *>(io), vbytes, keep_bytes()};
+    hsa_signal_store_relaxed(sig, 1);
+    {
+        std::lock_guard<std::mutex> lk(d.publish);
+        char *slot = d.karg + (size_t)(d.kslot.fetch_add(1, std::memory_order_relaxed) % kKargSlots) * kKargSlotBytes;
+        memcpy(slot, &ka, sizeof ka);
+        _mm_sfence();
+        *d.hdp = 1u;            // HDP flush: the BAR writes land in VRAM before the CP reads them
+        (void)*d.hdp;
+        hsa_queue_t *q = d.queue;
+        const uint64_t idx = hsa_queue_load_write_index_relaxed(q);
+        while (idx - hsa_queue_load_read_index_scacquire(q) >= q->size) _mm_pause();
+        hsa_kernel_dispatch_packet_t *p = (hsa_kernel_dispatch_packet_t *)q->base_address + (idx & (q->size - 1));
+        memset((char *)p + 4, 0, sizeof(*p) - 4);
+        p->workgroup_size_x = kThreads;
+        p->workgroup_size_y = 1;
+        p->workgroup_size_z = 1;
+        p->grid_size_x = groups * kThreads;
+        p->grid_size_y = 1;
+        p->grid_size_z = 1;
+        p->kernel_object = ko;
+        p->kernarg_address = slot;
+        p->completion_signal = sig;
+        const uint16_t header = (HSA_PACKET_TYPE_KERNEL_DISPATCH << HSA_PACKET_HEADER_TYPE) |
+                                (HSA_FENCE_SCOPE_AGENT << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE) |
+                                (HSA_FENCE_SCOPE_SYSTEM << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE);
+        const uint16_t setup = 1 << HSA_KERNEL_DISPATCH_PACKET_SETUP_DIMENSIONS;
+        hsa_queue_store_write_index_relaxed(q, idx + 1);
+        __atomic_store_n((uint32_t *)p, (uint32_t)header | ((uint32_t)setup << 16), __ATOMIC_RELEASE);
+        hsa_signal_store_screlease(q->doorbell_signal, idx);
+    }
+    for (uint64_t it = 1; hsa_signal_load_scacquire(sig) != 0; ++it) {
+        if ((it & 0xFFFF) == 0 && d.queue_error.load(std::memory_order_relaxed)) {
+            *rc = MPIR_HIP_ERUNTIME;
+            return 1;
+        }
+        _mm_pause();
+    }
+    g_direct_calls.fetch_add(1, std::memory_order_relaxed);
+    *rc = MPIR_HIP_OK;
+    return 1;
+}
+
+uint64_t direct_calls() { return g_direct_calls.load(std::memory_order_relaxed); }
+
+}  // namespace mpir_hip

@@ -28,6 +28,8 @@ namespace {
 }  // namespace
 
 namespace mpir_hip {
+int direct_reduce(int dev, int op, int elem, const void *in, void *io, uint64_t vbytes, int *rc);  // direct_dispatch.hip
+uint64_t direct_calls();
 Entry g_table[MPIR_HIP_NOPS][MPIR_HIP_NELEMS];
 multi_fn g_multi[MPIR_HIP_NOPS][MPIR_HIP_NELEMS][2][3];
 
@@ -91,6 +93,7 @@ struct DevCtx {
     hipEvent_t ev_up[kMaxStageSlots] = {}, ev_comp[kMaxStageSlots] = {}, ev_free[kMaxStageSlots] = {};
     volatile uint32_t *flag = nullptr;   // pinned completion word (wait mode "flag")
     uint32_t seq = 0;
+    bool main_pending = false;   // work enqueued on stream[S_MAIN] without a wait (stream variant)
     char *scratch = nullptr;     // staging slots x (in, inout) x chunk, or multi-operand temporaries
     size_t scratch_bytes = 0;
     char *bounce = nullptr;      // pinned host bounce slots x (in, inout) x chunk (pageable operands)
@@ -386,6 +389,8 @@ const char *MPIR_Hip_error_string(void) { return ctx().err; }
 
 uint64_t MPIR_Hip_host_max_bytes(void) { return host_max_bytes(); }
 
+uint64_t MPIR_Hip_direct_dispatches(void) { return direct_calls(); }
+
 int MPIR_Hip_thread_contexts(void) {
     std::lock_guard<std::mutex> lk(g_pool_mu);
     return g_ctx_created;
@@ -487,11 +492,30 @@ int MPIR_Hip_reduce(const void *inbuf, void *inoutbuf, uint64_t count, int op, i
         if (cur != dio) HIPCHK(hipSetDevice(dio));
         hipStream_t s = (hipStream_t)hip_stream;
         int rc = MPIR_HIP_OK;
+        DevCtx &d = ctx().dev[dio];
+        // synchronous, library stream, the lean tile shape: direct AQL dispatch
+        // (direct_dispatch.hip) when nothing queued on the library stream is
+        // still pending; otherwise, and for every other shape, the HIP launch
+        const uintptr_t ai = reinterpret_cast<uintptr_t>(inbuf), ao = reinterpret_cast<uintptr_t>(inoutbuf);
+        if (sync && !s && op != MPIR_HIP_OP_REPLACE && ((ai | ao) & 15) == 0 && ((count * esz) & 15) == 0) {
+            bool idle = !d.main_pending;
+            if (!idle && d.stream[S_MAIN] && hipStreamQuery(d.stream[S_MAIN]) == hipSuccess) {
+                d.main_pending = false;
+                idle = true;
+            }
+            (void)hipGetLastError();
+            if (idle && direct_reduce(dio, op, elem, inbuf, inoutbuf, count * esz, &rc)) {
+                if (rc != MPIR_HIP_OK) snprintf(ctx().err, sizeof(ctx().err), "direct dispatch: queue error");
+                if (cur != dio) (void)hipSetDevice(cur);
+                return rc;
+            }
+        }
         if (!s) rc = get_stream(dio, S_MAIN, &s);
         if (rc == MPIR_HIP_OK) {
             hipError_t e = fn(inbuf, inoutbuf, count * esz / unit, s);
             if (e != hipSuccess) rc = set_err(e, "kernel launch");
             else if (sync) rc = wait_stream(dio, s);
+            else if (!hip_stream) d.main_pending = true;
         }
         if (cur != dio) (void)hipSetDevice(cur);
         return rc;

@@ -660,3 +660,63 @@ def test_host_path_crossover(mpi, orc, cuda):
         esz = T.elem_size(t)
         for n in (lim // esz, lim // esz + 1):
             run_pair_host(mpi, orc, op, t, n, 21 + n)
+
+
+def _direct_count(mpi):
+    lib = mpi.load()
+    lib.MPIR_Hip_direct_dispatches.restype = ctypes.c_uint64
+    return lib.MPIR_Hip_direct_dispatches()
+
+
+def test_direct_dispatch_path(mpi, orc, cuda):
+    """Synchronous, aligned, device-resident calls of the hot (op, type) pairs
+    go through the direct AQL dispatch (direct_dispatch.hip); results bit-exact,
+    and shapes it does not take (head/tail elements, other ops) still right."""
+    torch = cuda
+    before = _direct_count(mpi)
+    for op, t in (("MPI_SUM", "MPI_FLOAT"), ("MPI_MAX", "MPI_DOUBLE"), ("MPI_PROD", "MPI_INT"),
+                  ("MPI_MIN", "MPIX_C_FLOAT16"), ("MPI_SUM", "MPI_C_DOUBLE_COMPLEX")):
+        run_pair(mpi, orc, torch, op, t, (1 << 18) + (16 // T.elem_size(t)) * 5, 31)
+    mid = _direct_count(mpi)
+    assert mid - before == 5, (before, mid)
+    run_pair(mpi, orc, torch, "MPI_SUM", "MPI_FLOAT", (1 << 18) + 1, 32)      # tail element: HIP launch
+    run_pair(mpi, orc, torch, "MPI_BXOR", "MPI_INT", 1 << 18, 33)            # op not in the code object
+    assert _direct_count(mpi) == mid
+
+
+def test_direct_dispatch_orders_after_null_stream(mpi, cuda):
+    """Work the caller left running on the legacy null stream for the operands
+    is finished before the reduction reads them (the direct path steps aside
+    while the null stream is busy)."""
+    torch = cuda
+    if torch.cuda.current_stream().cuda_stream != 0:
+        pytest.skip("torch's current stream is not the legacy null stream")
+    n = 1 << 24
+    src = torch.rand(n, device="cuda")
+    b = torch.rand(n, device="cuda")
+    a = torch.zeros(n, device="cuda")
+    big = torch.rand(4096, 4096, device="cuda")
+    torch.cuda.synchronize()
+    for _ in range(3):
+        big = big @ big / 4096.0          # keep the null stream busy for a while ...
+    a.copy_(src)                           # ... then produce the inout operand on it
+    rc = mpi.reduce_local(b.data_ptr(), a.data_ptr(), n, mpi.MPI_FLOAT, mpi.MPI_SUM)   # no sync before
+    assert rc == 0
+    want = (src + b).cpu().numpy()
+    assert np.array_equal(a.cpu().numpy(), want)
+
+
+def test_stream_variant_then_sync_call_ordered(mpi, cuda):
+    """MPIX_Reduce_local_stream on the library stream (hip_stream NULL, no wait)
+    then MPI_Reduce_local on the same buffers: the second call sees the first's
+    result ((a + b) + b, fp32 rounded twice)."""
+    torch = cuda
+    n = (1 << 22)
+    a0 = torch.rand(n, device="cuda")
+    b = torch.rand(n, device="cuda")
+    a = a0.clone()
+    torch.cuda.synchronize()
+    assert mpi.reduce_local_stream(b.data_ptr(), a.data_ptr(), n, mpi.MPI_FLOAT, mpi.MPI_SUM, 0) == 0
+    assert mpi.reduce_local(b.data_ptr(), a.data_ptr(), n, mpi.MPI_FLOAT, mpi.MPI_SUM) == 0
+    want = ((a0 + b) + b).cpu().numpy()
+    assert np.array_equal(a.cpu().numpy(), want)

@@ -67,6 +67,7 @@ struct Aql {
     int kslot = 0;
     volatile uint32_t *hdp = nullptr;
     uint16_t acq = HSA_FENCE_SCOPE_SYSTEM, rel = HSA_FENCE_SCOPE_SYSTEM;
+    int barrier = 1;
     void dispatch(uint64_t ko, uint32_t groups, const void *args, size_t nargs, bool with_signal) {
         char *ka = karg + (size_t)(kslot++ & 63) * 256;
         memcpy(ka, args, nargs);
@@ -83,7 +84,7 @@ struct Aql {
         p->kernarg_address = ka;
         p->completion_signal = with_signal ? sig : hsa_signal_t{0};
         const uint16_t header = (HSA_PACKET_TYPE_KERNEL_DISPATCH << HSA_PACKET_HEADER_TYPE) |
-                                (1 << HSA_PACKET_HEADER_BARRIER) |
+                                (barrier << HSA_PACKET_HEADER_BARRIER) |
                                 (acq << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE) |
                                 (rel << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE);
         const uint16_t setup = 1 << HSA_KERNEL_DISPATCH_PACKET_SETUP_DIMENSIONS;
@@ -233,20 +234,21 @@ int main(int argc, char **argv) {
     struct Var { std::string name; std::function<void(int, uint64_t *)> call; };
     std::vector<Var> vars;
     const char *only = getenv("AQL2_SWEEP");
+    // (declared here: the sweep's stored lambdas capture it by reference)
+    auto flagwait = [&]() {
+        CK(hipStreamWriteValue32(s, (void *)flag, ++seq, 0));
+        while (*flag != seq) __builtin_ia32_pause();
+    };
     if (only) {
         // store-mix sweep, HIP launch + completion word
-        auto flagwait = [&]() {
-            CK(hipStreamWriteValue32(s, (void *)flag, ++seq, 0));
-            while (*flag != seq) __builtin_ia32_pause();
-        };
-        for (int eighths : {0, 2, 3, 4, 5, 6, 7, 8}) {
-            const uint32_t from = grid - (uint32_t)((uint64_t)grid * eighths / 8);
-            vars.push_back({"tail_sc1_" + std::to_string(eighths) + "/8", [&, from](int i, uint64_t *t) {
+        for (int mib : {0, 32, 40, 48, 56, 64, 72, 80}) {
+            const uint32_t from = grid - (uint32_t)(((uint64_t)mib << 20) / 16384);
+            vars.push_back({"tail_sc1_" + std::to_string(mib) + "MiB", [&, from](int i, uint64_t *t) {
                 hipLaunchKernelGGL(a2_hyb, dim3(grid), dim3(256), 0, s, in(i), io(i), bytes, t, from);
                 flagwait();
             }});
         }
-        for (auto mk : std::vector<std::pair<int, int>>{{2, 1}, {4, 1}, {4, 2}, {8, 3}, {4, 3}, {16, 5}}) {
+        for (auto mk : std::vector<std::pair<int, int>>{}) {
             vars.push_back({"mod_sc1_" + std::to_string(mk.second) + "of" + std::to_string(mk.first),
                             [&, mk](int i, uint64_t *t) {
                 hipLaunchKernelGGL(a2_mod, dim3(grid), dim3(256), 0, s, in(i), io(i), bytes, t, (uint32_t)mk.first,
@@ -273,6 +275,16 @@ int main(int argc, char **argv) {
         }
     };
     const char *selfh = getenv("AQL2_SELFH");
+    {
+        const int N = 20000;
+        double t0 = now();
+        for (int i = 0; i < N; ++i) (void)hipStreamQuery(nullptr);
+        double t1 = now();
+        for (int i = 0; i < N; ++i) (void)hipStreamQuery(s);
+        double t2 = now();
+        printf("host hipStreamQuery(null) %.3f us, hipStreamQuery(own idle stream) %.3f us\n", (t1 - t0) / N * 1e6,
+               (t2 - t1) / N * 1e6);
+    }
     if (selfh) {
         const uint32_t from64 = grid - (uint32_t)((64ull << 20) / 16384);
         vars.push_back({"hip_flag_nt", [&](int i, uint64_t *t) {
@@ -285,7 +297,7 @@ int main(int argc, char **argv) {
             CK(hipStreamWriteValue32(s, (void *)flag, ++seq, 0));
             while (*flag != seq) __builtin_ia32_pause();
         }});
-        for (uint32_t from : {from64, grid - grid / 8, 0u}) {
+        for (uint32_t from : std::vector<uint32_t>{}) {
             vars.push_back({"hip_selfh_from" + std::to_string(from), [&, from](int i, uint64_t *t) {
                 const uint32_t q = ++seq;
                 hipLaunchKernelGGL(a2_selfh, dim3(grid), dim3(256), 0, s, in(i), io(i), bytes, t, ctl, (uint32_t *)flag, q,
@@ -293,13 +305,40 @@ int main(int argc, char **argv) {
                 selfwait(q, true);
             }});
         }
-        vars.push_back({"aql_selfh_agentacq_tail64M", [&](int i, uint64_t *t) {
+        if (0) vars.push_back({"aql_selfh_agentacq_tail64M", [&](int i, uint64_t *t) {
             const uint32_t q = ++seq;
             aq.acq = HSA_FENCE_SCOPE_AGENT;
             KaSelfh a{in(i), io(i), bytes, t, ctl, (uint32_t *)flag, q, grid, from64};
             aq.dispatch(ko_selfh, grid, &a, sizeof a, false);
             aq.acq = HSA_FENCE_SCOPE_SYSTEM;
             selfwait(q, false);
+        }});
+        vars.push_back({"aql_sig_tail64M_agentacq_nullq", [&](int i, uint64_t *t) {
+            // what the product would check first: is the legacy null stream idle?
+            if (hipStreamQuery(nullptr) != hipSuccess) { printf("null stream busy\n"); }
+            aq.acq = HSA_FENCE_SCOPE_AGENT;
+            KaHyb a{in(i), io(i), bytes, t, from64};
+            aq.dispatch(ko_hyb, grid, &a, sizeof a, true);
+            aq.wait();
+            aq.acq = HSA_FENCE_SCOPE_SYSTEM;
+        }});
+        vars.push_back({"aql_sig_tail64M_agentacq_agentrel", [&](int i, uint64_t *t) {
+            aq.acq = HSA_FENCE_SCOPE_AGENT;
+            aq.rel = HSA_FENCE_SCOPE_AGENT;
+            KaHyb a{in(i), io(i), bytes, t, from64};
+            aq.dispatch(ko_hyb, grid, &a, sizeof a, true);
+            aq.wait();
+            aq.acq = HSA_FENCE_SCOPE_SYSTEM;
+            aq.rel = HSA_FENCE_SCOPE_SYSTEM;
+        }});
+        vars.push_back({"aql_sig_tail64M_agentacq_nobarrier", [&](int i, uint64_t *t) {
+            aq.acq = HSA_FENCE_SCOPE_AGENT;
+            aq.barrier = 0;
+            KaHyb a{in(i), io(i), bytes, t, from64};
+            aq.dispatch(ko_hyb, grid, &a, sizeof a, true);
+            aq.wait();
+            aq.acq = HSA_FENCE_SCOPE_SYSTEM;
+            aq.barrier = 1;
         }});
         vars.push_back({"aql_sig_tail64M_agentacq", [&](int i, uint64_t *t) {
             aq.acq = HSA_FENCE_SCOPE_AGENT;
