@@ -175,6 +175,18 @@ int main(int argc, char **argv) {
             }
         }
         printf("kernarg probe: 200 dispatches saw their VRAM kernargs\n");
+        // host cost of the pieces of a dispatch
+        const int N = 20000;
+        double t0 = now();
+        for (int k = 0; k < N; ++k) { *aq.hdp = 1u; (void)*aq.hdp; }
+        double t1 = now();
+        for (int k = 0; k < N; ++k) { *aq.hdp = 1u; }
+        double t2 = now();
+        uint64_t vals[4] = {1, 2, 3, 4};
+        for (int k = 0; k < N; ++k) { memcpy(aq.karg + (k & 63) * 256, vals, 32); _mm_sfence(); }
+        double t3 = now();
+        printf("host: HDP flush + readback %.3f us, HDP flush write only %.3f us, 32 B kernarg BAR write + sfence %.3f us\n",
+               (t1 - t0) / N * 1e6, (t2 - t1) / N * 1e6, (t3 - t2) / N * 1e6);
     }
 
     hipStream_t s;
