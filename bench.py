@@ -16,11 +16,15 @@ torch.cuda.synchronize() on both sides, after W untimed warm-up steps.
             read inbuf, read inoutbuf, write inoutbuf -- SURVEY.md §8d)
 
 Extra fields (rank 0):
-  roofline      dominant kernel (k_reduce_tile_lean<OpSum,float>): algorithmic bytes per
+  roofline      dominant kernel: the synchronous call dispatches mpir_tile_SUM_MPIR_HIP_F32
+                on the library's own AQL queue (direct_dispatch.hip), which HIP
+                events cannot bracket; its HIP-launched twin k_reduce_tile_lean<OpSum,float>
+                (the same reduce_tile body) is timed instead: algorithmic bytes per
                 launch / mean launch duration from HIP events recorded on the
                 stream the kernel runs on (MPIX_Reduce_local_stream onto a torch
-                stream), vs the 8.0 TB/s HBM3E peak; traffic = per-launch HBM
-                bytes from the committed rocprofv3 PMC summary (profiles/) if present.
+                stream), vs the 8.0 TB/s HBM3E peak; rocprofv3 traces both kernels
+                (profiles/); traffic = per-launch HBM bytes from the committed
+                rocprofv3 PMC summary (profiles/) if present.
   stream_api    the same combine enqueued back-to-back with MPIX_Reduce_local_stream
                 (the async variant the library's own schedules use).
   pcie_inclusive  pinned host buffers -> MPI_Reduce_local (H2D + kernel + D2H),
@@ -387,9 +391,10 @@ def main():
         reduce_local, binding = lib.MPI_Reduce_local, "ctypes"
     dt_f32, op_sum = m.MPI_FLOAT, m.MPI_SUM
 
+    call_args = [(pin, pio, count, dt_f32, op_sum) for pin, pio in ptrs]
+
     def step(i):
-        pin, pio = ptrs[i % NPAIRS]
-        rc = reduce_local(pin, pio, count, dt_f32, op_sum)
+        rc = reduce_local(*call_args[i % NPAIRS])
         if rc:
             raise RuntimeError(m.error_string(rc))
 
@@ -444,7 +449,9 @@ def main():
         traffic, tsrc = load_traffic(nbytes)
         out["roofline"] = {
             "bound": "hbm",
-            "kernel": "mpir_hip::k_reduce_tile_lean<OpSum,float>",
+            "kernel": "mpir_tile_SUM_MPIR_HIP_F32 (the synchronous call's direct AQL dispatch); timed as its "
+                      "HIP-launched twin mpir_hip::k_reduce_tile_lean<OpSum,float>, the same reduce_tile<OpSum,float> "
+                      "body, on the stream it is launched on",
             "achieved": round(achieved / 1e9, 1),
             "peak": HBM_PEAK_BPS / 1e9,
             "unit": "GB/s",

@@ -15,6 +15,7 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <pthread.h>
 #include <stdint.h>
 
 #include "mpir_op_types.h"
@@ -69,13 +70,28 @@ static const MPIR_Type_desc type_table[] = {
     {MPI_LONG_DOUBLE_INT, MPIR_HIP_PLDOUBLEINT, G_LOC_PAIR, "MPI_LONG_DOUBLE_INT"},
 };
 
+/* Predefined handles are 0x4c00SSII (builtin, size SS, index II) or
+ * 0x8c00000I (the pair types): one table slot per (kind, II), filled once. */
+static const MPIR_Type_desc *by_index[2][256];
+static pthread_once_t by_index_once = PTHREAD_ONCE_INIT;
+
+static void by_index_init(void)
+{
+    for (size_t i = 0; i < sizeof(type_table) / sizeof(type_table[0]); i++) {
+        const unsigned h = (unsigned) type_table[i].datatype;
+        by_index[(h >> 24) == 0x8cu][h & 0xffu] = &type_table[i];
+    }
+}
+
 const MPIR_Type_desc *MPIR_Type_lookup(MPI_Datatype datatype)
 {
-    size_t i;
-    for (i = 0; i < sizeof(type_table) / sizeof(type_table[0]); i++)
-        if (type_table[i].datatype == datatype)
-            return &type_table[i];
-    return NULL;
+    const unsigned h = (unsigned) datatype;
+    const MPIR_Type_desc *d;
+    if ((h >> 24) != 0x4cu && (h >> 24) != 0x8cu)
+        return NULL;
+    pthread_once(&by_index_once, by_index_init);
+    d = by_index[(h >> 24) == 0x8cu][h & 0xffu];
+    return (d && d->datatype == datatype) ? d : NULL;
 }
 
 #define NUMERIC (G_C_INTEGER | G_C_INTEGER_EXTRA | G_FORTRAN_INTEGER | G_FLOATING_POINT | G_FLOATING_EXTRA)
