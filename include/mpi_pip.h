@@ -6,13 +6,17 @@
  * Ranks are processes started by mpich-pip_amd/bin/mpiexec (fork + exec);
  * they share one POSIX shared-memory segment that carries every transfer,
  * standing in for PiP's shared address space (pmip_cb.c:485-497).  Every
- * reduction step runs through MPIR_Reduce_local, i.e. the HIP kernels
- * (host operands are staged through the GPU; there is no CPU combine).
+ * reduction step runs through MPIR_Reduce_local: the HIP kernels, or, for
+ * host operands of at most MPIR_CVAR_REDUCE_LOCAL_HOST_MAX_KB, the same
+ * functors compiled for the host (csrc/hip/kernel_table.hpp); a builtin op
+ * with no HIP device is an error, never a CPU fallback.  Counts that differ
+ * across ranks give MPI_ERR_TRUNCATE / MPI_ERR_OTHER on the receiving ranks.
  *
  * Reference interfaces replaced (file:line under the reference tree):
  *   MPI_Comm, MPI_COMM_WORLD/SELF/NULL     src/include/mpi.h.in:89,289-291
  *   MPI_MAX_PROCESSOR_NAME (128)           configure.ac:5506
- *   MPI_ERR_COMM 5, MPI_ERR_ROOT 7         src/include/mpi.h.in:790-792
+ *   MPI_ERR_COMM 5, MPI_ERR_ROOT 7,        src/include/mpi.h.in:790-793
+ *   MPI_ERR_TRUNCATE 14
  *   MPI_Init / MPI_Finalize                src/mpi/init/init.c:118, finalize.c
  *   MPI_Comm_size / MPI_Comm_rank          src/mpi/comm/comm_size.c, comm_rank.c
  *   MPI_Get_processor_name, MPI_Wtime      src/mpi/misc/getpname.c, src/mpi/timer/wtime.c
@@ -40,6 +44,7 @@ typedef int MPI_Comm;
 #define MPI_MAX_PROCESSOR_NAME 128
 #define MPI_ERR_COMM  5
 #define MPI_ERR_ROOT  7
+#define MPI_ERR_TRUNCATE 14
 
 MPICH_API_PUBLIC int MPI_Init(int *argc, char ***argv);
 MPICH_API_PUBLIC int MPI_Initialized(int *flag);

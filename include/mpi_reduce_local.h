@@ -220,17 +220,20 @@ MPICH_API_PUBLIC int MPI_Error_string(int errorcode, char *string, int *resultle
  * as MPI_Reduce_local; user ops give MPI_ERR_OP (they run on the host). */
 MPICH_API_PUBLIC int MPIX_Reduce_local_stream(const void *inbuf, void *inoutbuf, int count, MPI_Datatype datatype,
                              MPI_Op op, void *hip_stream);
-/* Multi-operand local reduction: outbuf = fold of n device buffers in ONE pass
- * over HBM, in the association a reduction schedule would produce by calling
- * MPIR_Reduce_local step by step (bit-identical to doing exactly that):
+/* Multi-operand local reduction: outbuf = fold of n device buffers, in the
+ * association a reduction schedule would produce by calling MPIR_Reduce_local
+ * step by step (bit-identical to doing exactly that):
  *   MPIX_ORDER_TREE  (n a power of two <= 64): ((b0+b1)+(b2+b3))+((b4+b5)+(b6+b7)) --
  *       recursive halving, reduce_intra_reduce_scatter_gather.c:186-249;
  *   MPIX_ORDER_CHAIN (1 <= n <= 64): ((b0+b1)+b2)+... -- pairwise,
  *       reduce_scatter_block_intra_pairwise.c:97-134.
- * In each step the left operand is the step's inoutbuf.  outbuf may alias
- * inbufs[0].  hip_stream NULL: synchronous on the library stream; otherwise
- * enqueued on that stream without waiting.  Builtin ops and basic types with
- * the same validation as MPI_Reduce_local. */
+ * Passes over HBM: one for TREE (any n) and for CHAIN with n <= 8; CHAIN with
+ * n > 8 folds 7 more operands per pass into outbuf, ceil((n-1)/7) passes.
+ * In each step the left operand is the step's inoutbuf.  outbuf may be
+ * inbufs[0] exactly; any other overlap of outbuf with an operand is
+ * MPI_ERR_BUFFER.  hip_stream NULL: synchronous on the library stream;
+ * otherwise enqueued on that stream without waiting.  Builtin ops and basic
+ * types with the same validation as MPI_Reduce_local. */
 #define MPIX_ORDER_TREE  0
 #define MPIX_ORDER_CHAIN 1
 MPICH_API_PUBLIC int MPIX_Reduce_local_multi(const void *const *inbufs, int n, void *outbuf, int count,

@@ -104,6 +104,12 @@ uint64_t MPIR_Hip_host_max_bytes(void);
  * dispatch (direct_dispatch.hip) so far in this process (0 with
  * MPIR_CVAR_REDUCE_LOCAL_DISPATCH=hip or where the path is unavailable). */
 uint64_t MPIR_Hip_direct_dispatches(void);
+
+/* Kernel timing of the direct dispatch: with profiling on, the CP's start /
+ * end timestamps of each dispatch (as rocprofv3 reads them); the calling
+ * thread's last direct dispatch in ns (0 if none or profiling off). */
+void MPIR_Hip_direct_profile(int on);
+uint64_t MPIR_Hip_direct_last_kernel_ns(void);
 int MPIR_Hip_thread_contexts(void);
 
 #ifdef __cplusplus

@@ -93,6 +93,12 @@ struct DevState {
 
 DevState g_dev[kMaxDirectDev];
 std::atomic<uint64_t> g_direct_calls{0};
+// MPIX_Reduce_local_profile: the CP's start / end timestamps of each direct
+// dispatch (hsa_amd_profiling_get_dispatch_time, what rocprofv3 reads), so a
+// benchmark can time the kernel the synchronous call really runs
+std::atomic<int> g_profile{0};
+thread_local uint64_t t_last_kernel_ns = 0;
+uint64_t g_ts_freq = 0;
 
 int mode() {
     static const int m = [] {
@@ -248,6 +254,8 @@ void init_dev(int dev, DevState &d) {
         return;
     }
     d.agent = f.gpu;
+    if (g_profile.load()) hsa_amd_profiling_set_profiler_enabled(d.queue, 1);
+    if (!g_ts_freq) hsa_system_get_info(HSA_SYSTEM_INFO_TIMESTAMP_FREQUENCY, &g_ts_freq);
     d.karg = static_cast<char *>(kp);
     d.hdp = hdp.HDP_MEM_FLUSH_CNTL;
     d.ok = true;
@@ -368,11 +376,25 @@ int direct_reduce(int dev, int op, int elem, const void *in, void *io, uint64_t 
         _mm_pause();
     }
     if (held) held->inflight.fetch_sub(1, std::memory_order_acq_rel);
+    if (g_profile.load(std::memory_order_relaxed)) {
+        hsa_amd_profiling_dispatch_time_t t{};
+        t_last_kernel_ns = (hsa_amd_profiling_get_dispatch_time(d.agent, sig, &t) == HSA_STATUS_SUCCESS && g_ts_freq)
+                               ? (uint64_t)((double)(t.end - t.start) * 1e9 / (double)g_ts_freq)
+                               : 0;
+    }
     g_direct_calls.fetch_add(1, std::memory_order_relaxed);
     *rc = MPIR_HIP_OK;
     return 1;
 }
 
 uint64_t direct_calls() { return g_direct_calls.load(std::memory_order_relaxed); }
+
+void direct_profile(int on) {
+    g_profile.store(on ? 1 : 0);
+    for (int i = 0; i < kMaxDirectDev; ++i)
+        if (g_dev[i].ok) hsa_amd_profiling_set_profiler_enabled(g_dev[i].queue, on ? 1 : 0);
+}
+
+uint64_t direct_last_kernel_ns() { return t_last_kernel_ns; }
 
 }  // namespace mpir_hip

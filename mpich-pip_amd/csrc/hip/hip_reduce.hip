@@ -30,6 +30,8 @@ namespace {
 namespace mpir_hip {
 int direct_reduce(int dev, int op, int elem, const void *in, void *io, uint64_t vbytes, int *rc);  // direct_dispatch.hip
 uint64_t direct_calls();
+void direct_profile(int on);
+uint64_t direct_last_kernel_ns();
 Entry g_table[MPIR_HIP_NOPS][MPIR_HIP_NELEMS];
 multi_fn g_multi[MPIR_HIP_NOPS][MPIR_HIP_NELEMS][2][3];
 
@@ -390,6 +392,10 @@ const char *MPIR_Hip_error_string(void) { return ctx().err; }
 uint64_t MPIR_Hip_host_max_bytes(void) { return host_max_bytes(); }
 
 uint64_t MPIR_Hip_direct_dispatches(void) { return direct_calls(); }
+
+void MPIR_Hip_direct_profile(int on) { direct_profile(on); }
+
+uint64_t MPIR_Hip_direct_last_kernel_ns(void) { return direct_last_kernel_ns(); }
 
 int MPIR_Hip_thread_contexts(void) {
     std::lock_guard<std::mutex> lk(g_pool_mu);

@@ -225,6 +225,8 @@ static const char *class_string(int cls)
         return "Invalid MPI_Op";
     case MPI_ERR_ARG:
         return "Invalid argument";
+    case 14:   /* MPI_ERR_TRUNCATE */
+        return "Message truncated";
     case MPI_ERR_OTHER:
         return "Other MPI error";
     case MPI_ERR_INTERN:

@@ -341,6 +341,20 @@ int MPIX_Reduce_local_multi(const void *const *inbufs, int n, void *outbuf, int 
         MPIR_Err_set_detail("MPI_Op operation not defined for this datatype");
         return err_return(fc, MPI_ERR_OP);
     }
+    /* outbuf may be inbufs[0] exactly; any other overlap is refused whatever
+     * MPIR_CVAR_COLL_ALIAS_CHECK says: the CHAIN path for n > 8 writes outbuf
+     * between passes, before later operands are read */
+    {
+        const uintptr_t ob = (uintptr_t) outbuf;
+        const uintptr_t nb = (uintptr_t) count * MPIR_Hip_elem_size(elem);
+        for (j = 0; j < n; j++) {
+            const uintptr_t ib = (uintptr_t) inbufs[j];
+            if ((j > 0 || ib != ob) && ib < ob + nb && ob < ib + nb) {
+                MPIR_Err_set_detail("inbufs[%d] overlaps outbuf (only inbufs[0] may be outbuf, exactly)", j);
+                return err_return(fc, MPI_ERR_BUFFER);
+            }
+        }
+    }
     rc = MPIR_Hip_combine(inbufs, n, outbuf, (uint64_t) count, opidx, elem,
                           order == MPIX_ORDER_TREE ? MPIR_HIP_ORDER_TREE : MPIR_HIP_ORDER_CHAIN,
                           hip_stream, hip_stream == NULL);

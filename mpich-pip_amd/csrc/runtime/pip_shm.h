@@ -19,8 +19,9 @@
  * read across a recycle of the slot for another destination and lose a chunk. */
 typedef struct {
     _Atomic uint32_t owner;
-    uint32_t bytes;
-    char pad[56];
+    uint32_t bytes;             /* this chunk's bytes */
+    uint64_t total;             /* the whole message's bytes (every chunk carries it) */
+    char pad[48];
 } pip_slot_t;
 
 typedef struct {

@@ -64,15 +64,19 @@ static char *slot_data(int r)
     return (char *) W.shm + PIP_DATA_OFFSET + (size_t) r * PIP_CHUNK;
 }
 
-/* Send `sbytes` to `dst` and receive `rbytes` from `src` concurrently (either
- * side may be absent: dst / src < 0).  Progresses both directions chunk by
- * chunk so a pairwise exchange of long messages cannot deadlock. */
-static void sendrecv(const void *sbuf, size_t sbytes, int dst, void *rbuf, size_t rbytes, int src)
+/* Send `sbytes` to `dst` and receive up to `rbytes` from `src` concurrently
+ * (either side may be absent: dst / src < 0).  Progresses both directions
+ * chunk by chunk so a pairwise exchange of long messages cannot deadlock.
+ * Every chunk carries the message's total length, so the receiver takes
+ * exactly the message that was sent whatever it expected: a longer one is
+ * drained to its end with the excess dropped, a shorter one ends early.
+ * Returns the received message's length (0 with no receive side). */
+static size_t sendrecv(const void *sbuf, size_t sbytes, int dst, void *rbuf, size_t rbytes, int src)
 {
     pip_slot_t *mine = &W.shm->slot[W.rank];
     pip_slot_t *theirs = src >= 0 ? &W.shm->slot[src] : NULL;
-    size_t soff = 0, roff = 0;
-    int sdone = dst < 0, rdone = src < 0, sfirst = 1, rfirst = 1;
+    size_t soff = 0, roff = 0, rtotal = 0;
+    int sdone = dst < 0, rdone = src < 0, sfirst = 1;
     while (!sdone || !rdone) {
         int moved = 0;
         if (!sdone && atomic_load_explicit(&mine->owner, memory_order_acquire) == 0) {
@@ -80,6 +84,7 @@ static void sendrecv(const void *sbuf, size_t sbytes, int dst, void *rbuf, size_
             if (n)
                 memcpy(slot_data(W.rank), (const char *) sbuf + soff, n);
             mine->bytes = (uint32_t) n;
+            mine->total = sbytes;
             atomic_store_explicit(&mine->owner, (uint32_t) dst + 1, memory_order_release);
             soff += n;
             sfirst = 0;
@@ -87,15 +92,17 @@ static void sendrecv(const void *sbuf, size_t sbytes, int dst, void *rbuf, size_
             moved = 1;
         }
         if (!rdone && atomic_load_explicit(&theirs->owner, memory_order_acquire) == (uint32_t) W.rank + 1) {
-            size_t n = theirs->bytes;
-            if (roff + n > rbytes)      /* truncation: the message is longer than the receive buffer */
-                n = rbytes - roff;
-            if (n)
-                memcpy((char *) rbuf + roff, slot_data(src), n);
-            roff += theirs->bytes;
+            size_t n = theirs->bytes, keep = n;
+            rtotal = (size_t) theirs->total;
+            if (roff >= rbytes)
+                keep = 0;               /* truncation: past the end of the receive buffer */
+            else if (roff + n > rbytes)
+                keep = rbytes - roff;
+            if (keep)
+                memcpy((char *) rbuf + roff, slot_data(src), keep);
+            roff += n;
             atomic_store_explicit(&theirs->owner, 0, memory_order_release);
-            rfirst = 0;
-            rdone = roff >= rbytes && !rfirst;
+            rdone = roff >= rtotal;
             moved = 1;
         }
         if (!moved)
@@ -105,6 +112,33 @@ static void sendrecv(const void *sbuf, size_t sbytes, int dst, void *rbuf, size_
     if (dst >= 0)
         while (atomic_load_explicit(&mine->owner, memory_order_acquire) != 0)
             relax();
+    return rtotal;
+}
+
+/* A collective's first receive error, kept while the schedule runs on (as
+ * MPICH's errflag does, so no peer is left waiting) and returned at its end:
+ * a message longer than the receive buffer is MPI_ERR_TRUNCATE (MPIC_Recv,
+ * ch3u_request.c:516), any other length mismatch MPI_ERR_OTHER
+ * "**collective_size_mismatch" (bcast_intra_binomial.c:116-124). */
+static __thread int coll_err;
+static __thread char coll_why[160];
+
+static void note_length(size_t got, size_t want)
+{
+    if (got == want || coll_err)
+        return;
+    coll_err = got > want ? MPI_ERR_TRUNCATE : MPI_ERR_OTHER;
+    snprintf(coll_why, sizeof(coll_why), got > want ?
+             "Message truncated; %zu bytes received but buffer size is %zu" :
+             "message sizes do not match across processes in the collective routine: "
+             "Received %zu but expected %zu", got, want);
+}
+
+static void exchange(const void *sbuf, size_t sbytes, int dst, void *rbuf, size_t rbytes, int src)
+{
+    size_t got = sendrecv(sbuf, sbytes, dst, rbuf, rbytes, src);
+    if (src >= 0)
+        note_length(got, rbytes);
 }
 
 static void send_to(const void *buf, size_t bytes, int dst)
@@ -114,7 +148,21 @@ static void send_to(const void *buf, size_t bytes, int dst)
 
 static void recv_from(void *buf, size_t bytes, int src)
 {
-    sendrecv(NULL, 0, -1, buf, bytes, src);
+    note_length(sendrecv(NULL, 0, -1, buf, bytes, src), bytes);
+}
+
+/* the collective's result: its own error, else the first receive error */
+static int coll_finish(const char *fc, int rc)
+{
+    int e = coll_err;
+    coll_err = 0;
+    if (rc)
+        return rc;
+    if (e) {
+        MPIR_Err_set_detail("%s", coll_why);
+        return MPIR_Err_return(fc, e);
+    }
+    return MPI_SUCCESS;
 }
 
 /* ------------------------------------------------------------ init / finalize */
@@ -250,8 +298,8 @@ int MPI_Barrier(MPI_Comm comm)
     if (size == 1)
         return MPI_SUCCESS;
     for (mask = 1; mask < size; mask <<= 1)
-        sendrecv(NULL, 0, (rank + mask) % size, NULL, 0, (rank - mask + size) % size);
-    return MPI_SUCCESS;
+        exchange(NULL, 0, (rank + mask) % size, NULL, 0, (rank - mask + size) % size);
+    return coll_finish("MPI_Barrier", MPI_SUCCESS);
 }
 
 /* ------------------------------------------------------------ helpers */
@@ -299,7 +347,7 @@ int MPI_Bcast(void *buffer, int count, MPI_Datatype datatype, int root, MPI_Comm
     for (mask >>= 1; mask > 0; mask >>= 1)
         if (rel + mask < size)
             send_to(buffer, nbytes, (rank + mask) % size);
-    return MPI_SUCCESS;
+    return coll_finish(fc, MPI_SUCCESS);
 }
 
 /* ------------------------------------------------------------ Reduce */
@@ -405,7 +453,7 @@ static int reduce_scatter_gather(void *acc_, void *tmp_, int count, size_t esz, 
                 for (i = recv_idx; i < last_idx; i++)
                     recv_cnt += cnts[i];
             }
-            sendrecv(acc + (size_t) disps[send_idx] * esz, (size_t) send_cnt * esz, dst,
+            exchange(acc + (size_t) disps[send_idx] * esz, (size_t) send_cnt * esz, dst,
                      tmp + (size_t) disps[recv_idx] * esz, (size_t) recv_cnt * esz, dst);
             if ((rc = local_reduce("MPI_Reduce", tmp + (size_t) disps[recv_idx] * esz,
                                    acc + (size_t) disps[recv_idx] * esz, recv_cnt, dt, op)))
@@ -522,5 +570,5 @@ int MPI_Reduce(const void *sendbuf, void *recvbuf, int count, MPI_Datatype datat
         rc = reduce_binomial(acc, tmp, count, esz, datatype, op, root, rank, size);
     free(tmp);
     free(own);
-    return rc ? MPIR_Err_return(fc, rc) : MPI_SUCCESS;
+    return coll_finish(fc, rc ? MPIR_Err_return(fc, rc) : MPI_SUCCESS);
 }

@@ -5,6 +5,9 @@
  *
  *   argv[1] = "cpu": user-op reductions only (no GPU needed)
  *   argv[1] = "gpu": also builtin MPI_SUM reductions (HIP MPIR_Reduce_local)
+ *   argv[1] = "mismatch": collectives called with counts that differ across
+ *             ranks; every rank prints the error classes it got, then shows
+ *             the world still works (no rank is left waiting)
  */
 #include <stdint.h>
 #include <stdio.h>
@@ -46,6 +49,34 @@ int main(int argc, char **argv)
     MPI_Get_processor_name(name, &len);
     printf("hello %d %d %d\n", rank, size, len > 0);
     fflush(stdout);
+
+    if (argc > 1 && !strcmp(argv[1], "mismatch")) {
+        /* root 0 sends 2 MiB + 3 bytes (three chunks) where the others expect
+         * 1 MiB: longer than the receive buffer; then 100 bytes where the
+         * others expect 200: shorter; then a user-op MPI_Reduce where rank 1
+         * contributes 5 elements and everyone else (the root too) 3 */
+        const int big = (2 << 20) + 3, small = 1 << 20;
+        unsigned char *buf = calloc(big, 1);
+        uint32_t s5[5] = {1, 2, 3, 4, 5}, r5[5] = {0, 0, 0, 0, 0};
+        int c[3], x = rank == 0 ? 77 : 0;
+        MPI_Op op;
+        for (i = 0; i < big; i++)
+            buf[i] = rank == 0 ? (unsigned char) (i * 13) : 0;
+        MPI_Error_class(MPI_Bcast(buf, rank == 0 ? big : small, MPI_BYTE, 0, MPI_COMM_WORLD), &c[0]);
+        for (i = 0; i < small && (buf[i] == (unsigned char) (i * 13)); i++)
+            ;
+        flag = i == small && (rank == 0 || buf[small] == 0);        /* the excess was dropped */
+        MPI_Error_class(MPI_Bcast(buf, rank == 0 ? 100 : 200, MPI_BYTE, 0, MPI_COMM_WORLD), &c[1]);
+        MPI_Op_create(fp_op, 1, &op);
+        MPI_Error_class(MPI_Reduce(s5, r5, rank == 1 ? 5 : 3, MPI_UNSIGNED, op, 0, MPI_COMM_WORLD), &c[2]);
+        MPI_Op_free(&op);
+        MPI_Barrier(MPI_COMM_WORLD);
+        MPI_Bcast(&x, 1, MPI_INT, 0, MPI_COMM_WORLD);
+        printf("mismatch %d %d %d %d %d %d\n", rank, c[0], c[1], c[2], flag, x);
+        free(buf);
+        MPI_Finalize();
+        return 0;
+    }
 
     /* Bcast: 1 int and a 3 MiB + 5 byte buffer (multi-chunk) from every root */
     for (root = 0; root < size; root++) {

@@ -128,6 +128,21 @@ def test_in_place_rejected(mpi):
     assert mpi.reduce_local(IN_PLACE, a.ctypes.data, 0, mpi.MPI_FLOAT, mpi.MPI_SUM) == 0
 
 
+def test_multi_overlap_refused_before_any_device_work(mpi):
+    """MPIX_Reduce_local_multi refuses an outbuf overlapping any operand but
+    inbufs[0]-exactly, before it looks at residency (no GPU needed)."""
+    a = np.zeros(64, dtype=np.float32)
+    b = np.zeros(64, dtype=np.float32)
+    p = [a.ctypes.data, b.ctypes.data]
+    for out in (b.ctypes.data, b.ctypes.data + 8, a.ctypes.data + 4, b.ctypes.data - 4):
+        rc = mpi.reduce_local_multi(p, out, 64, mpi.MPI_FLOAT, mpi.MPI_SUM, mpi.MPIX_ORDER_CHAIN)
+        msg = mpi.error_string(rc)
+        assert mpi.error_class(rc) == mpi.MPI_ERR_BUFFER and ("overlaps outbuf" in msg or "aliased" in msg)
+    # exactly operand 0 passes the check (then host operands are refused as non-device)
+    rc = mpi.reduce_local_multi(p, a.ctypes.data, 64, mpi.MPI_FLOAT, mpi.MPI_SUM, mpi.MPIX_ORDER_CHAIN)
+    assert mpi.error_class(rc) == mpi.MPI_ERR_BUFFER and "overlaps" not in mpi.error_string(rc)
+
+
 def test_user_op_noncommutative_host(mpi):
     """test/mpi/coll/reduce_local.c: a non-commutative user op via MPI_Reduce_local
     (with the inout check the reference test forgot to reach)."""

@@ -1,15 +1,16 @@
-"""The committed bench line (profiles/r01s4_bench.log, measured on MI355X) against
+"""The committed bench line (profiles/r02_bench.log, measured on MI355X) against
 the driver's contract and against itself: BASELINE.json's metric, the
 required keys, value = algorithmic bytes x N / time, roofline.frac =
 achieved / peak with achieved = 805,306,368 B / mean launch time, and the
-PMC traffic it quotes equal to profiles/pmc_traffic.json."""
+PMC traffic it quotes equal to profiles/pmc_traffic.json, and its live
+launch time in agreement with the committed rocprofv3 average."""
 import json
 import os
 
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LINE = os.path.join(ROOT, "profiles", "r01s4_bench.log")
+LINE = os.path.join(ROOT, "profiles", "r02_bench.log")
 GIB = float(1 << 30)
 
 
@@ -55,3 +56,14 @@ def test_roofline_is_self_consistent(line):
         pmc = json.load(f)
     assert r["traffic"] == pmc["hbm_bytes_per_launch"]
     assert 1.0 <= r["traffic"] / r["algorithmic_bytes_per_launch"] < 1.01
+
+
+def test_live_kernel_time_agrees_with_rocprof(line):
+    """bench.py times the kernel the synchronous call runs; rocprofv3's
+    --kernel-trace --stats average for that kernel (profiles/r02_kernel_stats.csv,
+    summarised in pmc_traffic.json) must agree with it."""
+    r = line["roofline"]
+    with open(os.path.join(ROOT, "profiles", "pmc_traffic.json")) as f:
+        pmc = json.load(f)
+    assert "mpir_tile_SUM_MPIR_HIP_F32" in r["kernel"] and "mpir_tile_SUM_MPIR_HIP_F32" in pmc["kernel"]
+    assert r["mean_launch_us"] == pytest.approx(pmc["rocprof_avg_launch_ns"] * 1e-3, rel=0.05)

@@ -89,6 +89,25 @@ def test_plumbing_user_op(prog, n):
     assert rows["errs"][0] == ["7", "5", "2", "9"]
 
 
+@pytest.mark.parametrize("n", [2, 4])
+def test_mismatched_counts_error_not_hang(prog, n):
+    """A collective whose counts differ across ranks returns an error on the
+    receiving ranks instead of hanging (MPICH: MPIC_Recv MPI_ERR_TRUNCATE for a
+    longer message, "**collective_size_mismatch" MPI_ERR_OTHER for a shorter
+    one, bcast_intra_binomial.c:116-124), and the world stays usable."""
+    r = run(n, prog, "mismatch", timeout=60)
+    assert r.returncode == 0, r.stderr
+    rows = {int(v[0]): [int(x) for x in v[1:]] for v in parse(r.stdout)["mismatch"]}
+    assert sorted(rows) == list(range(n))
+    children = {m for m in (1, 2, 4) if m < n}          # root 0's binomial children
+    for rank, (long_, short, red, dropped, x) in rows.items():
+        assert long_ == (14 if rank in children else 0), rank      # MPI_ERR_TRUNCATE
+        assert short == (15 if rank in children else 0), rank      # MPI_ERR_OTHER
+        assert dropped == 1 and x == 77
+        # rank 1 sends 5 elements to rank 0 (its binomial parent), which expects 3
+        assert red == (14 if rank == 0 else 0), rank
+
+
 def test_builtin_reduce_without_gpu_fails_loudly(prog, mpi):
     if mpi.load().MPIR_Hip_device_count() > 0:
         pytest.skip("a GPU is visible: covered by test_pip_runtime_gpu.py")

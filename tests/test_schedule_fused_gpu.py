@@ -128,6 +128,31 @@ def test_multi_validation(mpi, cuda):
                                      mpi.MPIX_ORDER_CHAIN)) == mpi.MPI_ERR_BUFFER
 
 
+def test_multi_overlap_refused(mpi, cuda):
+    """outbuf may be inbufs[0] exactly; any other overlap is MPI_ERR_BUFFER,
+    whatever MPIR_CVAR_COLL_ALIAS_CHECK says (the CHAIN path for n > 8 writes
+    outbuf between passes)."""
+    torch = cuda
+    ec = mpi.error_class
+    bufs = [torch.full((4096,), float(j + 1), device="cuda") for j in range(12)]
+    p = [b.data_ptr() for b in bufs]
+    F, S, C, T = mpi.MPI_FLOAT, mpi.MPI_SUM, mpi.MPIX_ORDER_CHAIN, mpi.MPIX_ORDER_TREE
+    # exactly a later operand, on the multi-pass CHAIN shape and on a fused TREE
+    assert ec(mpi.reduce_local_multi(p, p[9], 4096, F, S, C)) == mpi.MPI_ERR_BUFFER
+    assert ec(mpi.reduce_local_multi(p[:4], p[2], 4096, F, S, T)) == mpi.MPI_ERR_BUFFER
+    # partial overlaps: with operand 0, and a later operand's tail
+    assert ec(mpi.reduce_local_multi(p[:4], p[0] + 16, 4096, F, S, T)) == mpi.MPI_ERR_BUFFER
+    assert ec(mpi.reduce_local_multi(p[:3], p[2] - 64, 4096, F, S, C)) == mpi.MPI_ERR_BUFFER
+    assert "overlaps outbuf" in mpi.error_string(mpi.reduce_local_multi(p[:3], p[1] + 4, 4096, F, S, C))
+    # adjacent (touching, not overlapping) and exactly operand 0 are fine
+    big = torch.ones(2 * 4096, device="cuda")
+    assert mpi.reduce_local_multi([big.data_ptr(), p[1]], big.data_ptr() + 4 * 4096, 4096, F, S, C) == 0
+    assert mpi.reduce_local_multi(p, p[0], 4096, F, S, C) == 0
+    torch.cuda.synchronize()
+    assert torch.equal(bufs[0], torch.full((4096,), float(sum(range(1, 13))), device="cuda"))
+    assert torch.equal(big[4096:], torch.full((4096,), 3.0, device="cuda"))
+
+
 ANY = [("MPI_DOUBLE_INT", "MPI_MINLOC"), ("MPI_2INT", "MPI_MAXLOC"), ("MPI_INT", "MPI_LAND"),
        ("MPI_UNSIGNED_SHORT", "MPI_BOR"), ("MPI_C_DOUBLE_COMPLEX", "MPI_PROD"), ("MPI_LONG_DOUBLE", "MPI_SUM"),
        ("MPI_LONG_DOUBLE_INT", "MPI_MAXLOC"), ("MPI_FLOAT", "MPI_SUM"), ("MPIX_C_FLOAT16", "MPI_MAX")]

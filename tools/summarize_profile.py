@@ -1,7 +1,12 @@
 #!/usr/bin/env python3
-"""Condense a rocprofv3 run of tools/profile_r01.sh into committed evidence.
+"""Condense a rocprofv3 run of tools/profile_r0N.sh into committed evidence.
 
-    python tools/summarize_profile.py gpurun_out/prof_r01 r01
+    python tools/summarize_profile.py gpurun_out/prof_r02 r02 [kernel-name-substring]
+
+The kernel defaults to the one the synchronous call dispatches since round 2
+(mpir_tile_SUM_MPIR_HIP_F32, direct AQL dispatch); round 1's runs used
+k_reduce_tile_lean<mpir_hip::OpSum, float>.  A trace64/ pass (config 2, 64 MiB
+per operand), when present, adds a second table.
 
 Writes, under profiles/:
   <tag>_kernel_stats.csv      rocprofv3 --stats kernel summary (names shortened)
@@ -20,7 +25,9 @@ import os
 import statistics
 import sys
 
-KERNEL = "k_reduce_tile_lean<mpir_hip::OpSum, float>"
+KERNEL = "mpir_tile_SUM_MPIR_HIP_F32"
+KERNEL_LABEL = {"mpir_tile_SUM_MPIR_HIP_F32": "mpir_tile_SUM_MPIR_HIP_F32 (reduce_tile<OpSum,float>, direct AQL dispatch)",
+                "k_reduce_tile_lean<mpir_hip::OpSum, float>": "mpir_hip::k_reduce_tile_lean<OpSum,float>"}
 PEAK = 8.0e12
 
 
@@ -30,6 +37,7 @@ def short(name: str) -> str:
 
 def main():
     src, tag = sys.argv[1], sys.argv[2]
+    kernel = sys.argv[3] if len(sys.argv) > 3 else KERNEL
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     prof = os.path.join(root, "profiles")
     os.makedirs(prof, exist_ok=True)
@@ -42,18 +50,18 @@ def main():
             r = dict(r)
             r["Name"] = short(r["Name"])
             w.writerow(r)
-    kstat = next(r for r in rows if KERNEL in r["Name"])
+    kstat = next(r for r in rows if kernel in r["Name"])
     avg_ns = float(kstat["AverageNs"])
 
     trace = [r for r in csv.DictReader(open(os.path.join(src, "trace", "run_kernel_trace.csv")))
-             if KERNEL in r["Kernel_Name"]]
+             if kernel in r["Kernel_Name"]]
     durs = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in trace]
 
     pmc = {}
     out_rows = []
     for name in ("fetch", "write"):
         for r in csv.DictReader(open(os.path.join(src, name, "run_counter_collection.csv"))):
-            if KERNEL in r["Kernel_Name"]:
+            if kernel in r["Kernel_Name"]:
                 pmc.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
                 out_rows.append({k: (short(v) if k == "Kernel_Name" else v) for k, v in r.items()})
     with open(os.path.join(prof, f"{tag}_pmc.csv"), "w", newline="") as f:
@@ -69,7 +77,7 @@ def main():
     hbm = int(round((2 * fetch_kb + write_kb) * 1024))
     achieved = alg / (avg_ns * 1e-9)
     d = {
-        "kernel": "mpir_hip::k_reduce_tile_lean<OpSum,float>",
+        "kernel": KERNEL_LABEL.get(kernel, kernel),
         "operand_bytes": operand_bytes,
         "algorithmic_bytes_per_launch": alg,
         "hbm_bytes_per_launch": hbm,
@@ -82,10 +90,31 @@ def main():
         "rocprof_frac_of_peak": round(achieved / PEAK, 4),
         "source": f"profiles/{tag}_kernel_stats.csv, profiles/{tag}_pmc.csv",
     }
+    t64 = os.path.join(src, "trace64", "run_kernel_stats.csv")
+    k64 = None
+    if os.path.exists(t64):
+        k64 = next(r for r in csv.DictReader(open(t64)) if kernel in r["Name"])
+        tr64 = [r for r in csv.DictReader(open(os.path.join(src, "trace64", "run_kernel_trace.csv")))
+                if kernel in r["Kernel_Name"]]
+        ob64 = int(tr64[0]["Grid_Size_X"]) // 256 * 16384
+        avg64 = float(k64["AverageNs"])
+        d["config2_64MiB"] = {"operand_bytes": ob64, "rocprof_avg_launch_ns": avg64,
+                              "rocprof_median_launch_ns": statistics.median(
+                                  int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in tr64),
+                              "rocprof_frac_of_peak": round(3 * ob64 / (avg64 * 1e-9) / PEAK, 4),
+                              "launches": int(k64["Calls"])}
+        with open(os.path.join(prof, f"{tag}_kernel_stats_64MiB.csv"), "w", newline="") as f:
+            rows64 = list(csv.DictReader(open(t64)))
+            w = csv.DictWriter(f, fieldnames=list(rows64[0].keys()))
+            w.writeheader()
+            for r in rows64:
+                r = dict(r)
+                r["Name"] = short(r["Name"])
+                w.writerow(r)
     json.dump(d, open(os.path.join(prof, "pmc_traffic.json"), "w"), indent=1)
     with open(os.path.join(prof, f"{tag}_summary.md"), "w") as f:
         f.write(f"# rocprofv3 summary ({tag})\n\n")
-        f.write("Command: `bash tools/profile_r01.sh` on one MI355X "
+        f.write(f"Command: `bash tools/profile_{tag[:3]}.sh` on one MI355X "
                 "(bench.py --no-cpu-baseline --no-extras: fp32 MPI_SUM, 256 MiB per operand).\n\n")
         f.write("| quantity | value |\n|---|---|\n")
         f.write(f"| kernel | `{d['kernel']}` |\n")
@@ -100,6 +129,14 @@ def main():
         f.write(f"| HBM traffic per launch | {hbm:,} B = {hbm/alg:.5f} x algorithmic |\n")
         f.write(f"| grid / workgroup / VGPR / SGPR | {grid // 256} WGs x 256, VGPR {trace[0]['VGPR_Count']}, "
                 f"SGPR {trace[0]['SGPR_Count']} |\n")
+        if k64 is not None:
+            c2 = d["config2_64MiB"]
+            f.write(f"\n## Config 2 (64 MiB per operand, `--mib 64`)\n\n| quantity | value |\n|---|---|\n")
+            f.write(f"| launches traced | {c2['launches']} |\n")
+            f.write(f"| average / median / min / max duration | {c2['rocprof_avg_launch_ns']/1e3:.2f} / "
+                    f"{c2['rocprof_median_launch_ns']/1e3:.2f} / {float(k64['MinNs'])/1e3:.2f} / "
+                    f"{float(k64['MaxNs'])/1e3:.2f} us |\n")
+            f.write(f"| achieved (algorithmic / average) | {c2['rocprof_frac_of_peak']:.3f} of 8.0 TB/s |\n")
     print(json.dumps(d, indent=1))
 
 
