@@ -110,6 +110,15 @@ uint64_t MPIR_Hip_direct_dispatches(void);
  * thread's last direct dispatch in ns (0 if none or profiling off). */
 void MPIR_Hip_direct_profile(int on);
 uint64_t MPIR_Hip_direct_last_kernel_ns(void);
+
+/* Direct-dispatch diagnostics: the device's state (0 not yet tried, 1 ready,
+ * -1..-10 the initialisation step that failed: properties, hsa_init, agents,
+ * VRAM pool, HDP register, code-object file, code-object load, kernel
+ * symbols, kernarg memory, queue; -20 disabled by
+ * MPIR_CVAR_REDUCE_LOCAL_DISPATCH=hip), and the number of direct calls that
+ * first synchronised with work reported pending on the legacy null stream. */
+int MPIR_Hip_direct_state(int dev);
+uint64_t MPIR_Hip_direct_busy_skips(void);
 int MPIR_Hip_thread_contexts(void);
 
 #ifdef __cplusplus

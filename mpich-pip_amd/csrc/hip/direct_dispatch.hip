@@ -80,6 +80,7 @@ struct CacheEntry {
 struct DevState {
     std::once_flag once;
     bool ok = false;
+    int state = 0;          // 0 not tried, 1 ready, < 0 the init step that failed (MPIR_Hip_direct_state)
     hsa_agent_t agent{};
     hsa_queue_t *queue = nullptr;
     char *karg = nullptr;                       // kKargSlots x kKargSlotBytes, VRAM, host-written
@@ -93,6 +94,7 @@ struct DevState {
 
 DevState g_dev[kMaxDirectDev];
 std::atomic<uint64_t> g_direct_calls{0};
+std::atomic<uint64_t> g_busy_skips{0};      // calls that first synchronised with a busy null stream
 // MPIX_Reduce_local_profile: the CP's start / end timestamps of each direct
 // dispatch (hsa_amd_profiling_get_dispatch_time, what rocprofv3 reads), so a
 // benchmark can time the kernel the synchronous call really runs
@@ -106,6 +108,16 @@ int mode() {
         return (e && !strcmp(e, "hip")) ? 0 : 1;
     }();
     return m;
+}
+
+// MPIR_CVAR_REDUCE_LOCAL_DIRECT_TIMESTAMPS (default 1): the direct queue
+// records dispatch start / end timestamps from its creation
+int timestamps() {
+    static const int t = [] {
+        const char *e = getenv("MPIR_CVAR_REDUCE_LOCAL_DIRECT_TIMESTAMPS");
+        return e ? (atoi(e) != 0) : 1;
+    }();
+    return t;
 }
 
 struct Find {
@@ -191,21 +203,27 @@ const char *elem_name(int e) {
 }
 
 void init_dev(int dev, DevState &d) {
+    d.state = -1;
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, dev) != hipSuccess) { (void)hipGetLastError(); return; }
     Find f;
     f.bdf = ((uint32_t)prop.pciBusID << 8) | ((uint32_t)prop.pciDeviceID << 3);
     f.domain = (uint32_t)prop.pciDomainID;
+    d.state = -2;
     if (hsa_init() != HSA_STATUS_SUCCESS) return;
     hsa_iterate_agents(find_agent, &f);
+    d.state = -3;
     if (!f.have_gpu || !f.have_cpu) return;
     hsa_amd_agent_iterate_memory_pools(f.gpu, find_vram, &f);
+    d.state = -4;
     if (!f.have_vram) return;
+    d.state = -5;
     hsa_amd_hdp_flush_t hdp{};
     if (hsa_agent_get_info(f.gpu, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_HDP_FLUSH, &hdp) != HSA_STATUS_SUCCESS ||
         !hdp.HDP_MEM_FLUSH_CNTL)
         return;
     // code object
+    d.state = -6;
     const std::string path = tiles_path();
     FILE *fp = path.empty() ? nullptr : fopen(path.c_str(), "rb");
     if (!fp) return;
@@ -214,6 +232,7 @@ void init_dev(int dev, DevState &d) {
     size_t n;
     while ((n = fread(buf, 1, sizeof buf, fp)) > 0) co.insert(co.end(), buf, buf + n);
     fclose(fp);
+    d.state = -7;
     hsa_code_object_reader_t rd;
     hsa_executable_t exe;
     if (hsa_code_object_reader_create_from_memory(co.data(), co.size(), &rd) != HSA_STATUS_SUCCESS) return;
@@ -222,6 +241,7 @@ void init_dev(int dev, DevState &d) {
         hsa_executable_load_agent_code_object(exe, f.gpu, rd, nullptr, nullptr) != HSA_STATUS_SUCCESS ||
         hsa_executable_freeze(exe, nullptr) != HSA_STATUS_SUCCESS)
         return;     // (the reader and executable live as long as the process)
+    d.state = -8;
     int found = 0;
     for (int op = 1; op < MPIR_HIP_NOPS; ++op) {
         for (int e = 1; e < MPIR_HIP_NELEMS; ++e) {
@@ -242,23 +262,29 @@ void init_dev(int dev, DevState &d) {
     }
     if (!found) return;
     // kernargs in VRAM, host-writable
+    d.state = -9;
     void *kp = nullptr;
     if (hsa_amd_memory_pool_allocate(f.vram, (size_t)kKargSlots * kKargSlotBytes, 0, &kp) != HSA_STATUS_SUCCESS) return;
     if (hsa_amd_agents_allow_access(1, &f.cpu, nullptr, kp) != HSA_STATUS_SUCCESS) {
         hsa_amd_memory_pool_free(kp);
         return;
     }
+    d.state = -10;
     if (hsa_queue_create(f.gpu, kQueueSize, HSA_QUEUE_TYPE_MULTI, queue_error_cb, &d, UINT32_MAX, UINT32_MAX,
                          &d.queue) != HSA_STATUS_SUCCESS) {
         hsa_amd_memory_pool_free(kp);
         return;
     }
     d.agent = f.gpu;
-    if (g_profile.load()) hsa_amd_profiling_set_profiler_enabled(d.queue, 1);
+    // dispatch timestamps on from the start: enabling them on a live queue
+    // takes effect only some time later (tools/direct_probe.py); they are read
+    // only while MPIR_Hip_direct_profile is on
+    if (timestamps()) hsa_amd_profiling_set_profiler_enabled(d.queue, 1);
     if (!g_ts_freq) hsa_system_get_info(HSA_SYSTEM_INFO_TIMESTAMP_FREQUENCY, &g_ts_freq);
     d.karg = static_cast<char *>(kp);
     d.hdp = hdp.HDP_MEM_FLUSH_CNTL;
     d.ok = true;
+    d.state = 1;
 }
 
 }  // namespace
@@ -309,10 +335,19 @@ int direct_reduce(int dev, int op, int elem, const void *in, void *io, uint64_t 
     if (!d.ok || d.queue_error.load(std::memory_order_relaxed)) return 0;
     const uint64_t ko = d.kobj[op][elem];
     if (!ko || vbytes == 0 || vbytes / 16384 >= (1ull << 26)) return 0;
-    // work queued on the legacy null stream stays ordered before us
+    // Work queued on the legacy null stream stays ordered before us, as it is
+    // for the HIP path's blocking library stream.  hipStreamQuery(nullptr)
+    // keeps answering "not ready" after such work has finished until the host
+    // synchronises with it (measured: tools/direct_probe.py), so a busy answer
+    // is followed by that synchronisation -- the wait the synchronous call
+    // would spend behind the same work on the HIP path anyway.
     if (hipStreamQuery(nullptr) != hipSuccess) {
         (void)hipGetLastError();
-        return 0;
+        g_busy_skips.fetch_add(1, std::memory_order_relaxed);
+        if (hipStreamSynchronize(nullptr) != hipSuccess) {
+            (void)hipGetLastError();
+            return 0;
+        }
     }
     hsa_signal_t sig;
     if (!t_sig.get(dev, &sig)) return 0;
@@ -391,10 +426,19 @@ uint64_t direct_calls() { return g_direct_calls.load(std::memory_order_relaxed);
 
 void direct_profile(int on) {
     g_profile.store(on ? 1 : 0);
-    for (int i = 0; i < kMaxDirectDev; ++i)
-        if (g_dev[i].ok) hsa_amd_profiling_set_profiler_enabled(g_dev[i].queue, on ? 1 : 0);
+    if (!timestamps())
+        for (int i = 0; i < kMaxDirectDev; ++i)
+            if (g_dev[i].ok) hsa_amd_profiling_set_profiler_enabled(g_dev[i].queue, on ? 1 : 0);
 }
 
 uint64_t direct_last_kernel_ns() { return t_last_kernel_ns; }
+
+int direct_state(int dev) {
+    if (mode() == 0) return -20;
+    if (dev < 0 || dev >= kMaxDirectDev) return -21;
+    return g_dev[dev].state;
+}
+
+uint64_t direct_busy_skips() { return g_busy_skips.load(std::memory_order_relaxed); }
 
 }  // namespace mpir_hip

@@ -32,6 +32,8 @@ int direct_reduce(int dev, int op, int elem, const void *in, void *io, uint64_t 
 uint64_t direct_calls();
 void direct_profile(int on);
 uint64_t direct_last_kernel_ns();
+int direct_state(int dev);
+uint64_t direct_busy_skips();
 Entry g_table[MPIR_HIP_NOPS][MPIR_HIP_NELEMS];
 multi_fn g_multi[MPIR_HIP_NOPS][MPIR_HIP_NELEMS][2][3];
 
@@ -396,6 +398,10 @@ uint64_t MPIR_Hip_direct_dispatches(void) { return direct_calls(); }
 void MPIR_Hip_direct_profile(int on) { direct_profile(on); }
 
 uint64_t MPIR_Hip_direct_last_kernel_ns(void) { return direct_last_kernel_ns(); }
+
+int MPIR_Hip_direct_state(int dev) { return direct_state(dev); }
+
+uint64_t MPIR_Hip_direct_busy_skips(void) { return direct_busy_skips(); }
 
 int MPIR_Hip_thread_contexts(void) {
     std::lock_guard<std::mutex> lk(g_pool_mu);

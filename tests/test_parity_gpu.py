@@ -686,8 +686,10 @@ def test_direct_dispatch_path(mpi, orc, cuda):
 
 def test_direct_dispatch_orders_after_null_stream(mpi, cuda):
     """Work the caller left running on the legacy null stream for the operands
-    is finished before the reduction reads them (the direct path steps aside
-    while the null stream is busy)."""
+    is finished before the reduction reads them: the direct path first
+    synchronises with a null stream that reports pending work, then dispatches
+    (hipStreamQuery(nullptr) alone keeps reporting finished work as pending
+    until the host synchronises, tools/direct_probe.py)."""
     torch = cuda
     if torch.cuda.current_stream().cuda_stream != 0:
         pytest.skip("torch's current stream is not the legacy null stream")
@@ -700,10 +702,39 @@ def test_direct_dispatch_orders_after_null_stream(mpi, cuda):
     for _ in range(3):
         big = big @ big / 4096.0          # keep the null stream busy for a while ...
     a.copy_(src)                           # ... then produce the inout operand on it
+    lib = mpi.load()
+    d0, s0 = _direct_count(mpi), lib.MPIR_Hip_direct_busy_skips()
     rc = mpi.reduce_local(b.data_ptr(), a.data_ptr(), n, mpi.MPI_FLOAT, mpi.MPI_SUM)   # no sync before
     assert rc == 0
+    assert _direct_count(mpi) == d0 + 1 and lib.MPIR_Hip_direct_busy_skips() == s0 + 1
     want = (src + b).cpu().numpy()
     assert np.array_equal(a.cpu().numpy(), want)
+
+
+def test_direct_dispatch_timestamps(mpi, cuda):
+    """MPIR_Hip_direct_profile: the first call after switching it on already
+    reports its kernel's CP start / end interval (the queue records timestamps
+    from its creation), and it lies within the call's own wall time."""
+    import time
+    torch = cuda
+    n = 1 << 24
+    a = torch.rand(n, device="cuda")
+    b = torch.rand(n, device="cuda")
+    torch.cuda.synchronize()
+    lib = mpi.load()
+    assert lib.MPIR_Hip_direct_state(torch.cuda.current_device()) in (0, 1)
+    assert mpi.reduce_local(b.data_ptr(), a.data_ptr(), n, mpi.MPI_FLOAT, mpi.MPI_SUM) == 0
+    assert lib.MPIR_Hip_direct_state(torch.cuda.current_device()) == 1
+    lib.MPIR_Hip_direct_profile(1)
+    try:
+        for _ in range(3):
+            t0 = time.perf_counter()
+            assert mpi.reduce_local(b.data_ptr(), a.data_ptr(), n, mpi.MPI_FLOAT, mpi.MPI_SUM) == 0
+            wall_ns = (time.perf_counter() - t0) * 1e9
+            ns = lib.MPIR_Hip_direct_last_kernel_ns()
+            assert 0 < ns < wall_ns, (ns, wall_ns)
+    finally:
+        lib.MPIR_Hip_direct_profile(0)
 
 
 def test_stream_variant_then_sync_call_ordered(mpi, cuda):
