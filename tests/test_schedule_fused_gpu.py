@@ -193,6 +193,56 @@ def test_one_pass_combine_matches_stepwise_fold(mpi, orc, cuda, t, op, n, order)
     assert same(out.cpu().numpy(), want, t)
 
 
+def test_concurrent_threads_minloc_tree16_regression(mpi, orc, cuda):
+    """Regression for the corruption removed in e7b5d60: several host threads
+    folding MPI_MINLOC (no fused kernel: the general path) at once, each on its
+    own library stream.  The removed path took its temporaries with
+    hipMallocAsync / hipFreeAsync, and the default memory pool handed a block
+    freed on one stream to another stream while the first stream's kernels
+    still read it (tools/mempool_race.hip: 3 of 1200 results corrupted at 4
+    threads, 14 of 2400 at 8; profiles/r02/mempool_race.log).  The product takes
+    no stream-ordered allocations (tests/test_no_stream_ordered_alloc_cpu.py);
+    this checks the concurrent folds stay bit-exact."""
+    import threading
+    torch = cuda
+    t, op, n, count, iters, nthreads = "MPI_DOUBLE_INT", "MPI_MINLOC", 16, 1 << 16, 12, 4
+    dt, o = mpi.DATATYPES[t], mpi.OPS[op]
+    esz = T.elem_size(t)
+    cases = []
+    for k in range(nthreads):
+        rng = np.random.default_rng(100 + k)
+        xs = [T.to_bytes(T.gen(t, count, rng, op)) for _ in range(n)]
+        acc = [x.copy() for x in xs]
+        step = 1
+        while step < n:
+            for j in range(0, n, 2 * step):
+                assert orc.reduce_local(acc[j + step], acc[j], count, dt, o, check=False) == 0
+            step *= 2
+        dev = [torch.from_numpy(x).cuda() for x in xs]
+        outs = [torch.zeros(count * esz, dtype=torch.uint8, device="cuda") for _ in range(iters)]
+        cases.append((acc[0], dev, outs))
+    torch.cuda.synchronize()
+    errors = []
+
+    def run(k):
+        want, dev, outs = cases[k]
+        for out in outs:
+            rc = mpi.reduce_local_multi([d.data_ptr() for d in dev], out.data_ptr(), count, dt, o,
+                                        mpi.MPIX_ORDER_TREE)
+            if rc:
+                errors.append(mpi.error_string(rc))
+    th = [threading.Thread(target=run, args=(k,)) for k in range(nthreads)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    assert not errors, errors
+    torch.cuda.synchronize()
+    for k, (want, _, outs) in enumerate(cases):
+        for i, out in enumerate(outs):
+            assert same(out.cpu().numpy(), want, t), (k, i)
+
+
 EVERY = [(op, t) for op in T.OPS for t in T.ALL_TYPES if T.compute_ok(op, t)]
 
 
