@@ -15,24 +15,31 @@ torch.cuda.synchronize() on both sides, after W untimed warm-up steps.
     value = 3 * 256 MiB * K * N / max_rank_seconds / 2^30   (GiB/s, algorithmic bytes:
             read inbuf, read inoutbuf, write inoutbuf -- SURVEY.md §8d)
 
+Runtime: HSA_ALLOCATE_QUEUE_DEV_MEM=1 (ROCm's knob for AQL rings in device
+memory, read once when the HSA runtime starts) unless the environment sets
+it: the CP then fetches each dispatch packet from VRAM instead of over PCIe,
+1.4 us off every synchronous call (profiles/r02/sync_ab_ring.log).
+The library's own launcher (bin/mpiexec) sets the same default for its ranks.
+
 Extra fields (rank 0):
-  roofline      dominant kernel: the synchronous call dispatches mpir_tile_SUM_MPIR_HIP_F32
-                on the library's own AQL queue (direct_dispatch.hip), which HIP
-                events cannot bracket; its HIP-launched twin k_reduce_tile_lean<OpSum,float>
-                (the same reduce_tile body) is timed instead: algorithmic bytes per
-                launch / mean launch duration from HIP events recorded on the
-                stream the kernel runs on (MPIX_Reduce_local_stream onto a torch
-                stream), vs the 8.0 TB/s HBM3E peak; rocprofv3 traces both kernels
-                (profiles/); traffic = per-launch HBM bytes from the committed
-                rocprofv3 PMC summary (profiles/) if present.
+  roofline      dominant kernel: mpir_tile_SUM_MPIR_HIP_F32, which the synchronous
+                call dispatches on the library's own AQL queue (direct_dispatch.hip);
+                its duration is the CP's dispatch start / end timestamps
+                (MPIR_Hip_direct_profile, the clock rocprofv3 reads), averaged over K
+                profiled repeats of the timed step; achieved = algorithmic bytes per
+                launch / that mean, vs the 8.0 TB/s HBM3E peak.  Its HIP-launched twin
+                k_reduce_tile_lean<OpSum,float> (same reduce_tile body), timed with HIP
+                events on its stream, is reported beside it; traffic = per-launch HBM
+                bytes from the committed rocprofv3 PMC summary (profiles/).
   stream_api    the same combine enqueued back-to-back with MPIX_Reduce_local_stream
                 (the async variant the library's own schedules use).
   pcie_inclusive  pinned host buffers -> MPI_Reduce_local (H2D + kernel + D2H),
                 the rate when rank buffers arrive in host memory over PiP shm.
                 Reported for DESIGN.md; never `value`.
-  cpu_baseline  the oracle's C loop (reference algorithm, gcc -O2) timed on every
-                physical core of this box, one pinned thread per core with NUMA-local
-                operands, on a bounded sample (rank 0, N = 1 only); per socket too.
+  cpu_baseline  the oracle's C loop (reference algorithm, gcc -O2) on this box's host
+                cores, one pinned thread per physical core (as many as the job's CPU
+                quota allows; every physical core as a secondary, throttled figure),
+                NUMA-local operands, a bounded sample (rank 0, N = 1 only); per socket.
 """
 from __future__ import annotations
 
@@ -43,6 +50,8 @@ import sys
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
+# before torch (or anything) starts the HSA runtime; see the docstring
+os.environ.setdefault("HSA_ALLOCATE_QUEUE_DEV_MEM", "1")
 sys.path.insert(0, os.path.join(ROOT, "mpich-pip_amd"))
 sys.path.insert(0, ROOT)
 
@@ -473,6 +482,7 @@ def main():
             "algorithmic_bytes_per_call": alg_bytes,
             "api": "MPI_Reduce_local (C ABI, synchronous; called through the " + binding + ")",
             "parallelism": "replica-per-gpu (no data-path collective)",
+            "runtime": {"HSA_ALLOCATE_QUEUE_DEV_MEM": os.environ.get("HSA_ALLOCATE_QUEUE_DEV_MEM", "")},
         },
         # the synchronous call per GPU (launch + completion included) against the HBM peak
         "per_gpu": {"GiBps": round(value / world, 1),

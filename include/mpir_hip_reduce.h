@@ -118,6 +118,10 @@ uint64_t MPIR_Hip_direct_last_kernel_ns(void);
  * MPIR_CVAR_REDUCE_LOCAL_DISPATCH=hip), and the number of direct calls that
  * first synchronised with work reported pending on the legacy null stream. */
 int MPIR_Hip_direct_state(int dev);
+/* With profiling on, the calling thread's last direct call on the system
+ * clock, ns from entering the dispatch: doorbell rung, CP start, CP end,
+ * completion seen by the host. */
+void MPIR_Hip_direct_last_split(uint64_t out[4]);
 uint64_t MPIR_Hip_direct_busy_skips(void);
 int MPIR_Hip_thread_contexts(void);
 

@@ -100,6 +100,15 @@ std::atomic<uint64_t> g_busy_skips{0};      // calls that first synchronised wit
 // benchmark can time the kernel the synchronous call really runs
 std::atomic<int> g_profile{0};
 thread_local uint64_t t_last_kernel_ns = 0;
+// with profiling on, the last direct call's timeline on the system clock, ns
+// from entering direct_reduce: doorbell rung, CP start, CP end, signal seen
+thread_local uint64_t t_last_split[4] = {};
+
+static inline uint64_t sys_ts() {
+    uint64_t t = 0;
+    hsa_system_get_info(HSA_SYSTEM_INFO_TIMESTAMP, &t);
+    return t;
+}
 uint64_t g_ts_freq = 0;
 
 int mode() {
@@ -118,6 +127,15 @@ int timestamps() {
         return e ? (atoi(e) != 0) : 1;
     }();
     return t;
+}
+
+// MPIR_CVAR_REDUCE_LOCAL_DIRECT_SIGNAL: "memory" (default, 0) or "interrupt" (1)
+int signal_kind() {
+    static const int k = [] {
+        const char *e = getenv("MPIR_CVAR_REDUCE_LOCAL_DIRECT_SIGNAL");
+        return (e && !strcmp(e, "interrupt")) ? 1 : 0;
+    }();
+    return k;
 }
 
 struct Find {
@@ -310,7 +328,14 @@ struct DirectSignals {
                 }
             }
             if (!have[dev]) {
-                if (hsa_signal_create(0, 0, nullptr, &sig[dev]) != HSA_STATUS_SUCCESS) return false;
+                // The host polls the signal and never sleeps on it, so it needs no
+                // interrupt event: naming the GPU as its only consumer makes ROCr
+                // create a plain memory signal (MPIR_CVAR_REDUCE_LOCAL_DIRECT_SIGNAL
+                // =interrupt keeps the default, event-backed kind)
+                hsa_status_t st;
+                if (signal_kind() == 0) st = hsa_signal_create(0, 1, &g_dev[dev].agent, &sig[dev]);
+                else st = hsa_signal_create(0, 0, nullptr, &sig[dev]);
+                if (st != HSA_STATUS_SUCCESS) return false;
                 have[dev] = true;
             }
         }
@@ -330,6 +355,9 @@ int direct_reduce(int dev, int op, int elem, const void *in, void *io, uint64_t 
     if (mode() == 0 || dev < 0 || dev >= kMaxDirectDev || op <= 0 || op >= MPIR_HIP_NOPS || elem <= 0 ||
         elem >= MPIR_HIP_NELEMS)
         return 0;
+    const bool prof = g_profile.load(std::memory_order_relaxed) != 0;
+    const uint64_t th0 = prof ? sys_ts() : 0;
+    uint64_t th1 = 0;
     DevState &d = g_dev[dev];
     std::call_once(d.once, [&] { init_dev(dev, d); });
     if (!d.ok || d.queue_error.load(std::memory_order_relaxed)) return 0;
@@ -352,7 +380,7 @@ int direct_reduce(int dev, int op, int elem, const void *in, void *io, uint64_t 
     hsa_signal_t sig;
     if (!t_sig.get(dev, &sig)) return 0;
     const uint32_t groups = (uint32_t)((vbytes + kTileBytes - 1) / kTileBytes);
-    const KArgs ka{static_cast<const char *>(in), static_cast<char *>(io), vbytes, keep_bytes()};
+    const KArgs ka{static_cast<const char *>(in), static_cast<char *>(io), vbytes, keep_for(vbytes)};
     hsa_signal_store_relaxed(sig, 1);
     CacheEntry *held = nullptr;
     {
@@ -401,6 +429,7 @@ int direct_reduce(int dev, int op, int elem, const void *in, void *io, uint64_t 
         const uint16_t setup = 1 << HSA_KERNEL_DISPATCH_PACKET_SETUP_DIMENSIONS;
         hsa_queue_store_write_index_relaxed(q, idx + 1);
         __atomic_store_n((uint32_t *)p, (uint32_t)header | ((uint32_t)setup << 16), __ATOMIC_RELEASE);
+        if (prof) th1 = sys_ts();
         hsa_signal_store_screlease(q->doorbell_signal, idx);
     }
     for (uint64_t it = 1; hsa_signal_load_scacquire(sig) != 0; ++it) {
@@ -411,11 +440,17 @@ int direct_reduce(int dev, int op, int elem, const void *in, void *io, uint64_t 
         _mm_pause();
     }
     if (held) held->inflight.fetch_sub(1, std::memory_order_acq_rel);
-    if (g_profile.load(std::memory_order_relaxed)) {
+    if (prof) {
+        const uint64_t th2 = sys_ts();
         hsa_amd_profiling_dispatch_time_t t{};
-        t_last_kernel_ns = (hsa_amd_profiling_get_dispatch_time(d.agent, sig, &t) == HSA_STATUS_SUCCESS && g_ts_freq)
-                               ? (uint64_t)((double)(t.end - t.start) * 1e9 / (double)g_ts_freq)
-                               : 0;
+        const bool okt = hsa_amd_profiling_get_dispatch_time(d.agent, sig, &t) == HSA_STATUS_SUCCESS && g_ts_freq;
+        const double ns = okt ? 1e9 / (double)g_ts_freq : 0.0;
+        t_last_kernel_ns = okt ? (uint64_t)((double)(t.end - t.start) * ns) : 0;
+        // the dispatch times are in the system domain, like HSA_SYSTEM_INFO_TIMESTAMP
+        t_last_split[0] = (uint64_t)((double)(th1 - th0) * ns);
+        t_last_split[1] = okt ? (uint64_t)((double)((int64_t)(t.start - th0)) * ns) : 0;
+        t_last_split[2] = okt ? (uint64_t)((double)((int64_t)(t.end - th0)) * ns) : 0;
+        t_last_split[3] = (uint64_t)((double)(th2 - th0) * ns);
     }
     g_direct_calls.fetch_add(1, std::memory_order_relaxed);
     *rc = MPIR_HIP_OK;
@@ -432,6 +467,10 @@ void direct_profile(int on) {
 }
 
 uint64_t direct_last_kernel_ns() { return t_last_kernel_ns; }
+
+void direct_last_split(uint64_t out[4]) {
+    for (int i = 0; i < 4; ++i) out[i] = t_last_split[i];
+}
 
 int direct_state(int dev) {
     if (mode() == 0) return -20;

@@ -33,6 +33,7 @@ uint64_t direct_calls();
 void direct_profile(int on);
 uint64_t direct_last_kernel_ns();
 int direct_state(int dev);
+void direct_last_split(uint64_t out[4]);
 uint64_t direct_busy_skips();
 Entry g_table[MPIR_HIP_NOPS][MPIR_HIP_NELEMS];
 multi_fn g_multi[MPIR_HIP_NOPS][MPIR_HIP_NELEMS][2][3];
@@ -48,6 +49,17 @@ uint64_t keep_bytes() {
         return (uint64_t)(mb >= 0 && mb <= 4096 ? mb : 64) << 20;
     }();
     return v;
+}
+
+uint64_t keep_for(uint64_t vbytes) {
+    // MPIR_CVAR_REDUCE_LOCAL_KEEP_MODE: "whole" (default) or "tail" (reduce_kernels.hpp)
+    static const bool tail = [] {
+        const char *e = getenv("MPIR_CVAR_REDUCE_LOCAL_KEEP_MODE");
+        return e && !strcmp(e, "tail");
+    }();
+    const uint64_t k = keep_bytes();
+    if (tail) return k;
+    return vbytes <= k ? vbytes : 0;
 }
 }  // namespace mpir_hip
 
@@ -400,6 +412,8 @@ void MPIR_Hip_direct_profile(int on) { direct_profile(on); }
 uint64_t MPIR_Hip_direct_last_kernel_ns(void) { return direct_last_kernel_ns(); }
 
 int MPIR_Hip_direct_state(int dev) { return direct_state(dev); }
+
+void MPIR_Hip_direct_last_split(uint64_t out[4]) { direct_last_split(out); }
 
 uint64_t MPIR_Hip_direct_busy_skips(void) { return direct_busy_skips(); }
 

@@ -36,24 +36,24 @@ constexpr int kVecPerLane = 4;
 constexpr uint32_t kTileBytes = kThreads * kVecPerLane * 16;  // 16 KiB per operand
 constexpr int kCachePolicyNT = 2;                             // aux bit: nt
 constexpr int kCachePolicySC1 = 16;                           // aux bit: sc1 (device scope)
-// The LAST `keep` bytes of every result (default kKeepBytes = 64 MiB; the
-// launchers pass keep_bytes(), i.e. MPIR_CVAR_REDUCE_LOCAL_KEEP_MB) are stored
-// with sc1 instead of nt.  An sc1 store allocates in the 256 MB Infinity Cache
-// (MALL), an nt store bypasses it.  Two effects, both measured on MI355X:
-//   * a result of at most 64 MiB stays in the MALL for its next reader (the
-//     next schedule step, the RCCL send of a block, the D2H copy of a staged
-//     chunk): 64 MiB re-read within ~256 MiB of traffic 27.0 vs 33.2 us
-//     (tools/sync_store_ab.hip, profiles/r01s4_sync_store_ab.log);
-//   * for a larger result, the write-back of its last 64 MiB drains from the
-//     MALL after the launch instead of inside it, so a synchronous call's
-//     kernel body ends earlier: 256 MiB fp32 SUM body 118.4-118.9 us vs
-//     120.6-121.1 (all nt), call 126.8-127.6 vs 128.8-129.4 us; the last
-//     96 MiB or more stored sc1 is slower than none (the MALL thrashes), and
-//     so is any mix spread over the whole launch (tools/aql/aql2.cpp,
-//     profiles/r02/store_tail_sweep.log).
+// Store policy (keep_for(), hip_reduce.hip): a result of at most `keep` bytes
+// (MPIR_CVAR_REDUCE_LOCAL_KEEP_MB, default kKeepBytes = 64 MiB) is stored with
+// sc1 instead of nt, a larger one nt.  An sc1 store allocates in the 256 MB
+// Infinity Cache (MALL), an nt store bypasses it; so a result of at most 64 MiB
+// stays there for its next reader (the next schedule step, the RCCL send of a
+// block, the D2H copy of a staged chunk): 64 MiB re-read within ~256 MiB of
+// traffic 27.0 vs 33.2 us (tools/sync_store_ab.hip,
+// profiles/r01s4_sync_store_ab.log).  With nothing re-read the two policies
+// are within noise at <= 64 MiB, and at 256 MiB sc1 on any part of the result
+// costs ~1 us (profiles/r02/pairs_ab.log: the "last 64 MiB sc1" variant,
+// MPIR_CVAR_REDUCE_LOCAL_KEEP_MODE=tail, only won where the bench's own
+// rotation let the next call but three re-read that tail from the MALL).
+// The kernels take the per-call `keep` and store sc1 the tiles in the last
+// `keep` bytes: keep = vbytes (all), 0 (none), or the tail mode's 64 MiB.
 // Nothing else changes: the bytes reach HBM either way (MALL is memory-side).
 constexpr uint64_t kKeepBytes = 64ull << 20;
-uint64_t keep_bytes();   // MPIR_CVAR_REDUCE_LOCAL_KEEP_MB, default kKeepBytes (hip_reduce.hip)
+uint64_t keep_bytes();               // MPIR_CVAR_REDUCE_LOCAL_KEEP_MB (hip_reduce.hip)
+uint64_t keep_for(uint64_t vbytes);  // the per-call `keep` argument of the kernels
 
 // true for a tile that starts inside the last `keep` bytes of a `vbytes` region
 __device__ __forceinline__ bool keep_tile(uint64_t base, uint64_t vbytes, uint64_t keep) {
@@ -86,7 +86,7 @@ struct TileArgs {
     const T *tail_in;   // elements after the vector region
     T *tail_io;
     uint32_t ntail;
-    uint64_t keep;      // keep_bytes(): the last `keep` bytes are stored sc1
+    uint64_t keep;      // keep_for(vbytes): the last `keep` bytes are stored sc1
 };
 
 template <class Op, class T>
@@ -323,7 +323,7 @@ hipError_t launch_reduce(const void *in_, void *io_, uint64_t count, hipStream_t
         a.tail_in = reinterpret_cast<const T *>(in + head_bytes + vbytes);
         a.tail_io = reinterpret_cast<T *>(io + head_bytes + vbytes);
         a.ntail = (uint32_t)((rest - vbytes) / sizeof(T));
-        a.keep = keep_bytes();
+        a.keep = keep_for(vbytes);
         uint64_t grid = (vbytes + kTileBytes - 1) / kTileBytes;
         if (grid == 0) grid = 1;
         if (a.nhead || a.ntail)
@@ -348,7 +348,7 @@ hipError_t launch_reduce(const void *in_, void *io_, uint64_t count, hipStream_t
         a.t.tail_in = reinterpret_cast<const T *>(in + head_bytes + vbytes);
         a.t.tail_io = reinterpret_cast<T *>(io + head_bytes + vbytes);
         a.t.ntail = (uint32_t)((rest - vbytes) / sizeof(T));
-        a.t.keep = keep_bytes();
+        a.t.keep = keep_for(vbytes);
         const uintptr_t vin = ai + head_bytes;
         a.delta = (uint32_t)(vin & 15);
         a.in_al = reinterpret_cast<const char *>(vin - a.delta);
@@ -436,7 +436,7 @@ hipError_t launch_reduce_wide(const void *in_, void *io_, uint64_t count, hipStr
         uint64_t grid = (nbytes + tile - 1) / tile;
         if (grid == 0) grid = 1;
         hipLaunchKernelGGL((k_reduce_tile_wide<Op, T, EPL>), dim3((unsigned)grid), dim3(kThreads), 0, s, in, io, nbytes,
-                           keep_bytes());
+                           keep_for(nbytes));
         return hipGetLastError();
     }
     uint64_t grid = (count + kThreads - 1) / kThreads;
@@ -471,7 +471,7 @@ struct MultiArgs {
     uint64_t vbytes;                // multiple of 16
     uint32_t nhead, ntail;          // scalar elements before / after the vector region
     int64_t head_off, tail_off;     // byte offsets of head / tail from the region starts
-    uint64_t keep;                  // keep_bytes()
+    uint64_t keep;                  // keep_for(vbytes)
 };
 
 template <class Op, class T, int P, bool TREE, bool RAW = false>
@@ -592,7 +592,6 @@ hipError_t launch_combine_pu(const void *const *ins, void *out_, uint64_t count,
     }
     MultiArgs a;
     for (int j = 0; j < kMaxOperands; ++j) a.in[j] = j < P ? static_cast<const char *>(ins[j]) : nullptr;
-    a.keep = keep_bytes();
     if (vec_ok) {
         uint64_t head = (16 - (ao & 15)) & 15;
         if (head > nbytes) head = nbytes;
@@ -600,6 +599,7 @@ hipError_t launch_combine_pu(const void *const *ins, void *out_, uint64_t count,
         for (int j = 0; j < P; ++j) a.in[j] += head;
         a.out = out + head;
         a.vbytes = vbytes;
+        a.keep = keep_for(vbytes);
         a.nhead = (uint32_t)(head / sizeof(T));
         a.head_off = -(int64_t)head;                // head elements sit before the region start
         a.ntail = (uint32_t)((rest - vbytes) / sizeof(T));
@@ -610,6 +610,7 @@ hipError_t launch_combine_pu(const void *const *ins, void *out_, uint64_t count,
     } else {
         a.out = out;
         a.vbytes = 0;
+        a.keep = 0;
         uint64_t grid = (count + kThreads - 1) / kThreads;
         if (grid > 4096) grid = 4096;
         if (grid == 0) grid = 1;
