@@ -129,6 +129,25 @@ int timestamps() {
     return t;
 }
 
+// packet fence scopes (experiments: MPIR_CVAR_REDUCE_LOCAL_DIRECT_ACQUIRE /
+// _RELEASE = none | agent | system); defaults agent acquire, system release
+static int scope_env(const char *name, int dflt) {
+    const char *e = getenv(name);
+    if (!e) return dflt;
+    if (!strcmp(e, "none")) return HSA_FENCE_SCOPE_NONE;
+    if (!strcmp(e, "agent")) return HSA_FENCE_SCOPE_AGENT;
+    if (!strcmp(e, "system")) return HSA_FENCE_SCOPE_SYSTEM;
+    return dflt;
+}
+int acquire_scope() {
+    static const int v = scope_env("MPIR_CVAR_REDUCE_LOCAL_DIRECT_ACQUIRE", HSA_FENCE_SCOPE_AGENT);
+    return v;
+}
+int release_scope() {
+    static const int v = scope_env("MPIR_CVAR_REDUCE_LOCAL_DIRECT_RELEASE", HSA_FENCE_SCOPE_SYSTEM);
+    return v;
+}
+
 // MPIR_CVAR_REDUCE_LOCAL_DIRECT_SIGNAL: "memory" (default, 0) or "interrupt" (1)
 int signal_kind() {
     static const int k = [] {
@@ -424,8 +443,8 @@ int direct_reduce(int dev, int op, int elem, const void *in, void *io, uint64_t 
         p->kernarg_address = slot;
         p->completion_signal = sig;
         const uint16_t header = (HSA_PACKET_TYPE_KERNEL_DISPATCH << HSA_PACKET_HEADER_TYPE) |
-                                (HSA_FENCE_SCOPE_AGENT << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE) |
-                                (HSA_FENCE_SCOPE_SYSTEM << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE);
+                                (acquire_scope() << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE) |
+                                (release_scope() << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE);
         const uint16_t setup = 1 << HSA_KERNEL_DISPATCH_PACKET_SETUP_DIMENSIONS;
         hsa_queue_store_write_index_relaxed(q, idx + 1);
         __atomic_store_n((uint32_t *)p, (uint32_t)header | ((uint32_t)setup << 16), __ATOMIC_RELEASE);

@@ -19,6 +19,9 @@
 #define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { \
     fprintf(stderr, "HIP %s at %s:%d\n", hipGetErrorString(e_), __FILE__, __LINE__); exit(2);} } while (0)
 
+namespace mpir_hip {
+uint64_t keep_bytes() { return getenv("KEEP_MB") ? strtoull(getenv("KEEP_MB"), 0, 10) << 20 : kKeepBytes; }
+}
 using namespace mpir_hip;
 
 // GAP: a gap after every GAP loads (0 = none)
@@ -56,7 +59,7 @@ __global__ __launch_bounds__(TH) void k_mx(MultiArgs a) {
             for (int j = 0; j < P; ++j) v[j] = pk[j].e[k];
             res.e[k] = fold_fast<OpSum, T, P, TREE>(v);
         }
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, res), ro, wb + u * 1024, 0, kCachePolicyNT);
+        store16(__builtin_bit_cast(u32x4, res), ro, wb + u * 1024, keep_tile(base, a.vbytes, a.keep));
     }
 }
 
@@ -117,6 +120,7 @@ hipError_t launch_mx(const void *const *ins, void *out, uint64_t count, hipStrea
     for (int j = 0; j < P; ++j) a.in[j] = static_cast<const char *>(ins[j]);
     a.out = static_cast<char *>(out);
     a.vbytes = count * sizeof(T);
+    a.keep = keep_bytes();
     constexpr uint32_t tile = TH * U * 16;
     hipLaunchKernelGGL((k_mx<T, TREE, P, U, TH, GAP>), dim3((unsigned)((a.vbytes + tile - 1) / tile)), dim3(TH), 0, s, a);
     return hipGetLastError();
@@ -145,14 +149,30 @@ int main(int argc, char **argv) {
     for (auto &p : outs) CK(hipMalloc(&p, bytes));
     // P = 2 / 4 shapes (the first P operands of a set); algorithmic bytes (P+1) x block
     // P = 8 (config 4 block at N = 8): longer contiguous runs per operand and wave
-    std::vector<Var> vs = {
+    const bool half = argc > 4 && atoi(argv[4]) == 16;
+    std::vector<Var> vs;
+    if (!half) vs = {
         {"TREE8 f32 product (U1 T1024)", 4, &launch_combine_p<OpSum, float, 8, true>},
+        {"TREE8 f32 U1 T256 gap4", 4, &launch_mx<float, true, 1, 256, 4>},
+        {"TREE8 f32 U1 T512 gap4", 4, &launch_mx<float, true, 1, 512, 4>},
+        {"TREE8 f32 U1 T1024 gap0", 4, &launch_mx<float, true, 1, 1024, 0>},
+        {"TREE8 f32 U1 T1024 gap2", 4, &launch_mx<float, true, 1, 1024, 2>},
+        {"TREE8 f32 U1 T1024 gap8", 4, &launch_mx<float, true, 1, 1024, 8>},
+        {"TREE8 f32 U2 T512 gap4", 4, &launch_mx<float, true, 2, 512, 4>},
         {"TREE8 f32 U2 T256 gap4", 4, &launch_mx<float, true, 2, 256, 4>},
-        {"TREE8 f32 U4 T256 gap4", 4, &launch_mx<float, true, 4, 256, 4>},
-        {"TREE8 f32 U4 T256 gap0", 4, &launch_mx<float, true, 4, 256, 0>},
-        {"TREE8 f32 U4 T128 gap4", 4, &launch_mx<float, true, 4, 128, 4>},
-        {"TREE8 f32 U2 T1024 gap4", 4, &launch_mx<float, true, 2, 1024, 4>},
     };
+    else vs = {
+        {"CHAIN8 f16 product (U1 T1024)", 2, &launch_combine_p<OpSum, _Float16, 8, false>},
+        {"CHAIN8 f16 U1 T256 gap4", 2, &launch_mx<_Float16, false, 1, 256, 4>},
+        {"CHAIN8 f16 U1 T512 gap4", 2, &launch_mx<_Float16, false, 1, 512, 4>},
+        {"CHAIN8 f16 U1 T1024 gap0", 2, &launch_mx<_Float16, false, 1, 1024, 0>},
+        {"CHAIN8 f16 U1 T1024 gap8", 2, &launch_mx<_Float16, false, 1, 1024, 8>},
+        {"CHAIN8 f16 U2 T512 gap4", 2, &launch_mx<_Float16, false, 2, 512, 4>},
+    };
+    std::vector<std::vector<float>> dur(vs.size());
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
     hipStream_t st;
     CK(hipStreamCreate(&st));
     std::vector<int> order(vs.size());
@@ -168,10 +188,22 @@ int main(int argc, char **argv) {
             const int s = slot++ % NS;
             const void *ptr[P];
             for (int j = 0; j < P; ++j) ptr[j] = ins[s * P + j];
+            CK(hipEventRecord(e0, st));
             CK(vs[vi].fn(ptr, outs[s], bytes / vs[vi].esz, st));
+            CK(hipEventRecord(e1, st));
             CK(hipStreamSynchronize(st));
+            float ms = 0;
+            CK(hipEventElapsedTime(&ms, e0, e1));
+            if (r >= 0) dur[vi].push_back(ms * 1e3f);
         }
     }
-    printf("8 x %zu MiB -> 1 (operand stride %zu B), %d rounds; durations: see the rocprofv3 kernel trace\n", mib, bytes + skew, rounds);
+    printf("8 x %zu MiB -> 1 (operand stride %zu B), %d rounds; HIP-event medians (the rocprofv3 trace has the kernel times)\n",
+           mib, bytes + skew, rounds);
+    for (size_t i = 0; i < vs.size(); ++i) {
+        std::sort(dur[i].begin(), dur[i].end());
+        const float med = dur[i][dur[i].size() / 2];
+        printf("  %-34s median %7.2f us  p10 %7.2f  frac %.4f\n", vs[i].name.c_str(), med, dur[i][dur[i].size() / 10],
+               9.0 * bytes / (med * 1e-6) / 8e12);
+    }
     return 0;
 }
