@@ -137,6 +137,10 @@ def main():
                     f"{c2['rocprof_median_launch_ns']/1e3:.2f} / {float(k64['MinNs'])/1e3:.2f} / "
                     f"{float(k64['MaxNs'])/1e3:.2f} us |\n")
             f.write(f"| achieved (algorithmic / average) | {c2['rocprof_frac_of_peak']:.3f} of 8.0 TB/s |\n")
+            f.write("\n`--mib 64` rotates the bench's 4 pairs, and results of at most 64 MiB are stored `sc1`\n"
+                    "(they stay in the 256 MB Infinity Cache), so each call re-reads its inout from the\n"
+                    "cache four calls later: this is a cache figure, not config 2. Config 2 proper (16\n"
+                    "windows over 2 GiB, nothing re-read) is `config2_64MiB` in the bench line.\n")
     print(json.dumps(d, indent=1))
 
 
