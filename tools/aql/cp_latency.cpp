@@ -12,6 +12,9 @@
 //               second's CP start minus the first's CP end
 //   barrier+d   an empty barrier-AND packet rung first, the dispatch rung d us
 //               later: its doorbell -> CP start
+//   spinner     a one-wave kernel (tools/aql/spin_kernel.hip, argv[2]) already
+//               running and polling a flag word; the call publishes its
+//               dispatch behind it, rings, then sets the flag: flag -> CP start
 #include <hsa/hsa.h>
 #include <hsa/hsa_ext_amd.h>
 #include <immintrin.h>
@@ -56,6 +59,18 @@ static hsa_status_t find_kern(hsa_amd_memory_pool_t p, void *) {
     uint32_t f = 0;
     hsa_amd_memory_pool_get_info(p, HSA_AMD_MEMORY_POOL_INFO_GLOBAL_FLAGS, &f);
     if ((f & HSA_AMD_MEMORY_POOL_GLOBAL_FLAG_KERNARG_INIT) && !g_have_kern) { g_kern = p; g_have_kern = true; }
+    return HSA_STATUS_SUCCESS;
+}
+
+static hsa_amd_memory_pool_t g_fine;
+static bool g_have_fine = false;
+static hsa_status_t find_fine(hsa_amd_memory_pool_t p, void *) {
+    hsa_amd_segment_t seg;
+    hsa_amd_memory_pool_get_info(p, HSA_AMD_MEMORY_POOL_INFO_SEGMENT, &seg);
+    if (seg != HSA_AMD_SEGMENT_GLOBAL) return HSA_STATUS_SUCCESS;
+    uint32_t f = 0;
+    hsa_amd_memory_pool_get_info(p, HSA_AMD_MEMORY_POOL_INFO_GLOBAL_FLAGS, &f);
+    if ((f & HSA_AMD_MEMORY_POOL_GLOBAL_FLAG_FINE_GRAINED) && !g_have_fine) { g_fine = p; g_have_fine = true; }
     return HSA_STATUS_SUCCESS;
 }
 
@@ -176,8 +191,10 @@ int main(int argc, char **argv) {
     printf("HSA_ALLOCATE_QUEUE_DEV_MEM=%s\n", getenv("HSA_ALLOCATE_QUEUE_DEV_MEM") ? getenv("HSA_ALLOCATE_QUEUE_DEV_MEM") : "(unset)");
 
     const int K = 300;
+    const bool spin_only = getenv("SPIN_ONLY") != nullptr;
     // idle G
     for (double G : {0.0, 5.0, 20.0, 100.0, 1000.0}) {
+        if (spin_only) break;
         std::vector<double> d2s, s2e, e2h;
         for (int k = 0; k < K + 10; ++k) {
             spin_us(G);
@@ -279,6 +296,100 @@ int main(int argc, char **argv) {
             }
             printf("parked barrier (%.0f us): release->CP start %5.2f; publish -> host sees %5.2f\n", pre, med(r2s),
                    med(tot));
+        }
+    }
+    // spinner: needs the spin kernel's code object
+    if (argc > 2) {
+        hsa_amd_agent_iterate_memory_pools(g_cpu, find_fine, nullptr);
+        FILE *f2 = fopen(argv[2], "rb");
+        if (!f2 || !g_have_fine) { printf("no spin code object / fine-grained pool\n"); return 0; }
+        std::vector<char> co2;
+        while ((n = fread(buf, 1, sizeof buf, f2)) > 0) co2.insert(co2.end(), buf, buf + n);
+        fclose(f2);
+        hsa_code_object_reader_t rd2;
+        hsa_executable_t exe2;
+        HK(hsa_code_object_reader_create_from_memory(co2.data(), co2.size(), &rd2));
+        HK(hsa_executable_create_alt(HSA_PROFILE_FULL, HSA_DEFAULT_FLOAT_ROUNDING_MODE_DEFAULT, nullptr, &exe2));
+        HK(hsa_executable_load_agent_code_object(exe2, g_gpu, rd2, nullptr, nullptr));
+        HK(hsa_executable_freeze(exe2, nullptr));
+        hsa_executable_symbol_t sym2;
+        HK(hsa_executable_get_symbol_by_name(exe2, "spin_wait.kd", &g_gpu, &sym2));
+        uint64_t ko_spin = 0;
+        HK(hsa_executable_symbol_get_info(sym2, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_OBJECT, &ko_spin));
+        // flag in host fine-grained memory, or (SPIN_FLAG_VRAM=1) in VRAM written
+        // through the BAR and pushed by an HDP flush; spinner kernargs in the kernarg pool
+        const bool vram_flag = getenv("SPIN_FLAG_VRAM") != nullptr;
+        uint32_t *flag = nullptr;
+        volatile uint32_t *hdp = nullptr;
+        if (vram_flag) {
+            HK(hsa_amd_memory_pool_allocate(g_vram, 4096, 0, (void **)&flag));
+            HK(hsa_amd_agents_allow_access(1, &g_cpu, nullptr, flag));
+            hsa_amd_hdp_flush_t h{};
+            HK(hsa_agent_get_info(g_gpu, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_HDP_FLUSH, &h));
+            hdp = h.HDP_MEM_FLUSH_CNTL;
+        } else {
+            HK(hsa_amd_memory_pool_allocate(g_fine, 4096, 0, (void **)&flag));
+            HK(hsa_amd_agents_allow_access(1, &g_gpu, nullptr, flag));
+        }
+        printf("spinner flag in %s\n", vram_flag ? "VRAM (BAR write + HDP flush)" : "host fine-grained memory");
+        void *karg2 = nullptr;
+        HK(hsa_amd_memory_pool_allocate(g_kern, 64, 0, &karg2));
+        HK(hsa_amd_agents_allow_access(1, &g_gpu, nullptr, karg2));
+        struct { const uint32_t *f; uint64_t max_ticks; } sa{flag, 100000ull};   // 1 ms at 100 MHz
+        memcpy(karg2, &sa, sizeof sa);
+        hsa_signal_t ss;
+        HK(hsa_signal_create(0, 1, &g_gpu, &ss));
+        for (double pre : {5.0, 20.0}) {
+            std::vector<double> f2s, gap, tot;
+            int timeouts = 0;
+            for (int k = 0; k < K + 10; ++k) {
+                __atomic_store_n(flag, 0u, __ATOMIC_RELEASE);
+                if (hdp) { _mm_sfence(); *hdp = 1u; (void)*hdp; }
+                hsa_signal_store_relaxed(ss, 1);
+                hsa_signal_store_relaxed(s1, 1);
+                uint64_t idx = hsa_queue_load_write_index_relaxed(g_q);
+                {   // the spinner
+                    hsa_kernel_dispatch_packet_t *p = (hsa_kernel_dispatch_packet_t *)g_q->base_address + (idx & (g_q->size - 1));
+                    memset((char *)p + 4, 0, sizeof(*p) - 4);
+                    p->workgroup_size_x = 64;
+                    p->workgroup_size_y = 1;
+                    p->workgroup_size_z = 1;
+                    p->grid_size_x = 64;
+                    p->grid_size_y = 1;
+                    p->grid_size_z = 1;
+                    p->kernel_object = ko_spin;
+                    p->kernarg_address = karg2;
+                    p->completion_signal = ss;
+                    const uint16_t header = (HSA_PACKET_TYPE_KERNEL_DISPATCH << HSA_PACKET_HEADER_TYPE) |
+                                            (HSA_FENCE_SCOPE_AGENT << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE) |
+                                            (HSA_FENCE_SCOPE_AGENT << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE);
+                    const uint16_t setup = 1 << HSA_KERNEL_DISPATCH_PACKET_SETUP_DIMENSIONS;
+                    hsa_queue_store_write_index_relaxed(g_q, idx + 1);
+                    __atomic_store_n((uint32_t *)p, (uint32_t)header | ((uint32_t)setup << 16), __ATOMIC_RELEASE);
+                    hsa_signal_store_screlease(g_q->doorbell_signal, idx);
+                }
+                spin_us(pre);                       // the spinner is running now
+                const uint64_t t0 = ts();
+                write_dispatch(idx + 1, s1, true);
+                hsa_queue_store_write_index_relaxed(g_q, idx + 2);
+                hsa_signal_store_screlease(g_q->doorbell_signal, idx + 1);
+                const uint64_t tf = ts();
+                __atomic_store_n(flag, 1u, __ATOMIC_RELEASE);
+                if (hdp) { _mm_sfence(); *hdp = 1u; }
+                wait(s1);
+                const uint64_t t1 = ts();
+                wait(ss);
+                uint64_t a, b, sa0, sb0;
+                times(s1, &a, &b);
+                times(ss, &sa0, &sb0);
+                if (k < 10) continue;
+                if (us(sb0 - sa0) > 900.0) ++timeouts;
+                f2s.push_back(us(a - tf));
+                gap.push_back(us(a - sb0));
+                tot.push_back(us(t1 - t0));
+            }
+            printf("spinner (%.0f us ahead): flag -> CP start %5.2f; spinner end -> CP start %5.2f; publish -> host sees %5.2f"
+                   " (timeouts %d)\n", pre, med(f2s), med(gap), med(tot), timeouts);
         }
     }
     return 0;
