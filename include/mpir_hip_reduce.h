@@ -100,6 +100,12 @@ int MPIR_Hip_device_count(void);
  * are host memory (MPIR_CVAR_REDUCE_LOCAL_HOST_MAX_KB, default 1 MiB). */
 uint64_t MPIR_Hip_host_max_bytes(void);
 
+/* One operand host memory, the other on a device, at most this many bytes
+ * (MPIR_CVAR_REDUCE_LOCAL_MIXED_MAX_KB, default 1 MiB): the host operand is
+ * copied into the calling thread's pinned, device-mapped slot and the kernel
+ * reads (writes) it there directly; larger calls use the staging pipeline. */
+uint64_t MPIR_Hip_mixed_max_bytes(void);
+
 /* Synchronous device-resident reductions completed through the direct AQL
  * dispatch (direct_dispatch.hip) so far in this process (0 with
  * MPIR_CVAR_REDUCE_LOCAL_DISPATCH=hip or where the path is unavailable). */

@@ -114,6 +114,8 @@ struct DevCtx {
     size_t scratch_bytes = 0;
     char *bounce = nullptr;      // pinned host bounce slots x (in, inout) x chunk (pageable operands)
     size_t bounce_bytes = 0;
+    char *zc = nullptr;          // pinned, device-mapped slot for small mixed-residency calls
+    size_t zc_bytes = 0;
 };
 
 struct ThreadCtx {
@@ -312,6 +314,38 @@ uint64_t host_max_bytes() {
     return v;
 }
 
+// One operand in host memory, the other on a device, at most this many bytes:
+// the host operand is copied into a pinned, device-mapped slot and the kernel
+// reads (and for a host inoutbuf writes) it there over PCIe -- one dispatch, no
+// DMA copies, no staging pipeline.  Measured fp32 SUM host -> device at count 1:
+// 33 us through the staged pipeline (profiles/r02/host_latency.log).
+// MPIR_CVAR_REDUCE_LOCAL_MIXED_MAX_KB (default 1024; 0 = always stage).
+uint64_t mixed_max_bytes() {
+    static const uint64_t v = [] {
+        const char *e = getenv("MPIR_CVAR_REDUCE_LOCAL_MIXED_MAX_KB");
+        const long kb = e ? atol(e) : 1024;
+        return (uint64_t)(kb >= 0 && kb <= (1L << 20) ? kb : 1024) << 10;
+    }();
+    return v;
+}
+
+// the calling thread's small pinned slot (fine-grained: kernel stores land in
+// host memory without a cache flush)
+int get_zc(int dev, size_t bytes, char **out) {
+    DevCtx &d = ctx().dev[dev];
+    if (d.zc_bytes < bytes) {
+        // a synchronous call's kernel is done with the old slot when it returned
+        if (d.zc) HIPCHK(hipHostFree(d.zc));
+        d.zc = nullptr;
+        d.zc_bytes = 0;
+        const size_t want = bytes < ((size_t)64 << 10) ? ((size_t)64 << 10) : bytes;
+        HIPCHK(hipHostMalloc(&d.zc, want, hipHostMallocCoherent | hipHostMallocMapped));
+        d.zc_bytes = want;
+    }
+    *out = d.zc;
+    return MPIR_HIP_OK;
+}
+
 // page-locked host memory (hipHostMalloc / hipHostRegister): DMA-able as is
 bool is_pinned_host(const void *p) {
     hipPointerAttribute_t at;
@@ -388,6 +422,48 @@ int wait_stream(int dev, hipStream_t s) {
     return MPIR_HIP_OK;
 }
 
+// Both operands reachable by device `dev`'s kernels (device memory, or the
+// pinned slot of the mixed path): direct AQL dispatch for a synchronous call
+// on the library stream with the lean tile shape, when nothing queued on the
+// library stream is still pending; otherwise, and for every other shape, the
+// HIP launch (then the wait, for a synchronous call).
+int device_call(int dev, const void *inbuf, void *inoutbuf, uint64_t count, int op, int elem, hipStream_t user_s,
+                int sync) {
+    launch_fn fn = g_table[op][elem].fn;
+    const size_t esz = g_elem_size[elem];
+    // REPLACE is registered as a byte copy: its launcher counts bytes
+    const uint64_t unit = (op == MPIR_HIP_OP_REPLACE) ? 1 : esz;
+    int cur = 0;
+    HIPCHK(hipGetDevice(&cur));
+    if (cur != dev) HIPCHK(hipSetDevice(dev));
+    hipStream_t s = user_s;
+    int rc = MPIR_HIP_OK;
+    DevCtx &d = ctx().dev[dev];
+    const uintptr_t ai = reinterpret_cast<uintptr_t>(inbuf), ao = reinterpret_cast<uintptr_t>(inoutbuf);
+    if (sync && !s && op != MPIR_HIP_OP_REPLACE && ((ai | ao) & 15) == 0 && ((count * esz) & 15) == 0) {
+        bool idle = !d.main_pending;
+        if (!idle && d.stream[S_MAIN] && hipStreamQuery(d.stream[S_MAIN]) == hipSuccess) {
+            d.main_pending = false;
+            idle = true;
+        }
+        (void)hipGetLastError();
+        if (idle && direct_reduce(dev, op, elem, inbuf, inoutbuf, count * esz, &rc)) {
+            if (rc != MPIR_HIP_OK) snprintf(ctx().err, sizeof(ctx().err), "direct dispatch: queue error");
+            if (cur != dev) (void)hipSetDevice(cur);
+            return rc;
+        }
+    }
+    if (!s) rc = get_stream(dev, S_MAIN, &s);
+    if (rc == MPIR_HIP_OK) {
+        hipError_t e = fn(inbuf, inoutbuf, count * esz / unit, s);
+        if (e != hipSuccess) rc = set_err(e, "kernel launch");
+        else if (sync) rc = wait_stream(dev, s);
+        else if (!user_s) d.main_pending = true;
+    }
+    if (cur != dev) (void)hipSetDevice(cur);
+    return rc;
+}
+
 }  // namespace
 
 extern "C" {
@@ -404,6 +480,8 @@ int MPIR_Hip_has_kernel(int op, int elem) {
 const char *MPIR_Hip_error_string(void) { return ctx().err; }
 
 uint64_t MPIR_Hip_host_max_bytes(void) { return host_max_bytes(); }
+
+uint64_t MPIR_Hip_mixed_max_bytes(void) { return mixed_max_bytes(); }
 
 uint64_t MPIR_Hip_direct_dispatches(void) { return direct_calls(); }
 
@@ -512,40 +590,8 @@ int MPIR_Hip_reduce(const void *inbuf, void *inoutbuf, uint64_t count, int op, i
     const Loc lio = classify(inoutbuf, &dio);
 
     // ---- fast path: both operands device-resident on one device ----------
-    if (lin == LOC_DEVICE && lio == LOC_DEVICE && din == dio) {
-        int cur = 0;
-        HIPCHK(hipGetDevice(&cur));
-        if (cur != dio) HIPCHK(hipSetDevice(dio));
-        hipStream_t s = (hipStream_t)hip_stream;
-        int rc = MPIR_HIP_OK;
-        DevCtx &d = ctx().dev[dio];
-        // synchronous, library stream, the lean tile shape: direct AQL dispatch
-        // (direct_dispatch.hip) when nothing queued on the library stream is
-        // still pending; otherwise, and for every other shape, the HIP launch
-        const uintptr_t ai = reinterpret_cast<uintptr_t>(inbuf), ao = reinterpret_cast<uintptr_t>(inoutbuf);
-        if (sync && !s && op != MPIR_HIP_OP_REPLACE && ((ai | ao) & 15) == 0 && ((count * esz) & 15) == 0) {
-            bool idle = !d.main_pending;
-            if (!idle && d.stream[S_MAIN] && hipStreamQuery(d.stream[S_MAIN]) == hipSuccess) {
-                d.main_pending = false;
-                idle = true;
-            }
-            (void)hipGetLastError();
-            if (idle && direct_reduce(dio, op, elem, inbuf, inoutbuf, count * esz, &rc)) {
-                if (rc != MPIR_HIP_OK) snprintf(ctx().err, sizeof(ctx().err), "direct dispatch: queue error");
-                if (cur != dio) (void)hipSetDevice(cur);
-                return rc;
-            }
-        }
-        if (!s) rc = get_stream(dio, S_MAIN, &s);
-        if (rc == MPIR_HIP_OK) {
-            hipError_t e = fn(inbuf, inoutbuf, count * esz / unit, s);
-            if (e != hipSuccess) rc = set_err(e, "kernel launch");
-            else if (sync) rc = wait_stream(dio, s);
-            else if (!hip_stream) d.main_pending = true;
-        }
-        if (cur != dio) (void)hipSetDevice(cur);
-        return rc;
-    }
+    if (lin == LOC_DEVICE && lio == LOC_DEVICE && din == dio)
+        return device_call(dio, inbuf, inoutbuf, count, op, elem, (hipStream_t)hip_stream, sync);
     if (!sync) return MPIR_HIP_EBUFFER;  // the stream variant needs device buffers
 
     // ---- small, both host-resident: combine on this thread --------------
@@ -553,6 +599,28 @@ int MPIR_Hip_reduce(const void *inbuf, void *inoutbuf, uint64_t count, int op, i
         if (MPIR_Hip_device_count() == 0) return MPIR_HIP_ENODEV;
         g_table[op][elem].host(inbuf, inoutbuf, count * esz / unit);
         return MPIR_HIP_OK;
+    }
+
+    // ---- small, one operand host memory and the other on a device: the host
+    // ---- operand goes through the thread's pinned slot, which the kernel
+    // ---- reads (writes) directly; the slot copy keeps the device operand's
+    // ---- offset mod 256 so the aligned tile kernels still apply
+    if ((lin == LOC_DEVICE) != (lio == LOC_DEVICE) && count * esz <= mixed_max_bytes()) {
+        const uint64_t bytes = count * esz;
+        const int dev = lin == LOC_DEVICE ? din : dio;
+        const uintptr_t adev = reinterpret_cast<uintptr_t>(lin == LOC_DEVICE ? inbuf : (const void *)inoutbuf);
+        char *slot = nullptr;
+        int rc = get_zc(dev, (size_t)bytes + 256, &slot);
+        if (rc != MPIR_HIP_OK) return rc;
+        slot += adev & 255;
+        if (lio == LOC_DEVICE) {
+            memcpy(slot, inbuf, bytes);
+            return device_call(dev, slot, inoutbuf, count, op, elem, nullptr, 1);
+        }
+        memcpy(slot, inoutbuf, bytes);
+        rc = device_call(dev, inbuf, slot, count, op, elem, nullptr, 1);
+        if (rc == MPIR_HIP_OK) memcpy(inoutbuf, slot, bytes);
+        return rc;
     }
 
     // ---- staged path: at least one operand is host memory (or the two ----

@@ -662,6 +662,81 @@ def test_host_path_crossover(mpi, orc, cuda):
             run_pair_host(mpi, orc, op, t, n, 21 + n)
 
 
+def run_pair_mixed(mpi, orc, torch, op, t, n, seed, host_side, pinned=False, off_host=0, off_dev=0):
+    """One operand in host memory (`host_side` "in" or "inout"; pageable numpy or
+    pinned torch memory, at byte offset `off_host`), the other on the device."""
+    rng = np.random.default_rng(seed)
+    a = T.to_bytes(T.gen(t, n, rng, op))          # inout
+    b = T.to_bytes(T.gen(t, n, rng, op))          # in
+    want = a.copy()
+    rc_o = orc.reduce_local(b.copy(), want, n, mpi.DATATYPES[t], mpi.OPS[op])
+
+    def host(x):
+        if pinned:
+            h = torch.zeros(x.size + off_host, dtype=torch.uint8).pin_memory()
+            h[off_host:] = torch.from_numpy(x)
+            return h, h.data_ptr() + off_host
+        h = np.zeros(x.size + off_host, np.uint8)
+        h[off_host:] = x
+        return h, h.ctypes.data + off_host
+
+    def host_back(h, size):
+        return (h.numpy() if pinned else h)[off_host:off_host + size].copy()
+    if host_side == "in":
+        hin, pin = host(b)
+        tio, pio = dev(torch, a, off_dev)
+        rc = mpi.reduce_local(pin, pio, n, mpi.DATATYPES[t], mpi.OPS[op])
+        got = back(tio, off_dev, a.size)
+        assert np.array_equal(host_back(hin, b.size), b), "inbuf modified"
+    else:
+        tin, pin = dev(torch, b, off_dev)
+        hio, pio = host(a)
+        rc = mpi.reduce_local(pin, pio, n, mpi.DATATYPES[t], mpi.OPS[op])
+        got = host_back(hio, a.size)
+        assert np.array_equal(back(tin, off_dev, b.size), b), "inbuf modified"
+    assert mpi.error_class(rc) == rc_o, (op, t, rc, rc_o)
+    if not same(got, want, t):
+        pytest.fail(f"mixed ({host_side} on host, pinned={pinned}) {op} {t} n={n} off=({off_host},{off_dev}):\n"
+                    + explain(got, want, a, b, T.elem_size(t)))
+
+
+MIXED = [("MPI_SUM", "MPI_FLOAT"), ("MPI_MAX", "MPI_DOUBLE"), ("MPI_PROD", "MPI_INT"), ("MPI_SUM", "MPIX_C_FLOAT16"),
+         ("MPI_BXOR", "MPI_UNSIGNED_CHAR"), ("MPI_MINLOC", "MPI_DOUBLE_INT"), ("MPI_PROD", "MPI_C_DOUBLE_COMPLEX"),
+         ("MPI_LAND", "MPI_SHORT"), ("MPI_SUM", "MPI_LONG_DOUBLE"), ("MPI_MAXLOC", "MPI_LONG_DOUBLE_INT")]
+
+
+@pytest.mark.parametrize("op,t", MIXED, ids=[f"{o}-{t}" for o, t in MIXED])
+def test_mixed_small_path_vs_oracle(mpi, orc, cuda, op, t):
+    """One operand host memory, the other device memory, below
+    MPIR_Hip_mixed_max_bytes: the host operand goes through the thread's pinned
+    slot that the kernel reads / writes directly.  Both directions, pageable and
+    pinned host memory, aligned and misaligned, ragged counts; bit-exact."""
+    for side in ("in", "inout"):
+        for pinned in (False, True):
+            for n, seed, oh, od in ((1, 41, 0, 0), (7, 42, 3, 0), (1000, 43, 0, 16), (4099, 44, 5, 8),
+                                    (65536 + 3, 45, 0, 0)):
+                run_pair_mixed(mpi, orc, cuda, op, t, n, seed, side, pinned, oh, od)
+
+
+def test_mixed_path_crossover(mpi, orc, cuda):
+    """Either side of MPIR_Hip_mixed_max_bytes (pinned slot below, staging
+    pipeline above), both directions: bit-exact; below it the direct dispatch
+    runs (aligned fp32 SUM)."""
+    lib = mpi.load()
+    lib.MPIR_Hip_mixed_max_bytes.restype = ctypes.c_uint64
+    lim = lib.MPIR_Hip_mixed_max_bytes()
+    assert lim == 1 << 20
+    for op, t in (("MPI_SUM", "MPI_FLOAT"), ("MPI_MAXLOC", "MPI_DOUBLE_INT")):
+        esz = T.elem_size(t)
+        for side in ("in", "inout"):
+            for n in (lim // esz, lim // esz + 1):
+                run_pair_mixed(mpi, orc, cuda, op, t, n, 51 + n, side)
+    d0 = _direct_count(mpi)
+    run_pair_mixed(mpi, orc, cuda, "MPI_SUM", "MPI_FLOAT", 4096, 60, "in")
+    run_pair_mixed(mpi, orc, cuda, "MPI_SUM", "MPI_FLOAT", 4096, 61, "inout")
+    assert _direct_count(mpi) == d0 + 2
+
+
 def _direct_count(mpi):
     lib = mpi.load()
     lib.MPIR_Hip_direct_dispatches.restype = ctypes.c_uint64

@@ -5,7 +5,7 @@ and count, against the reference's CPU loop on the same host buffers.
     python3 tools/host_latency.py [--reps 200]
 
 Residencies: pageable host -> pageable host, pinned -> pinned, host in -> device
-inout, device -> device.  CPU loop: the oracle's restatement of opsum.c's loop
+inout, pinned in -> device inout, device in -> host inout, device -> device.  CPU loop: the oracle's restatement of opsum.c's loop
 (gcc -O2), timed here as the reference point only (tools/, never the product).
 Prints one line per (residency, count): median / p10 / p90 microseconds per call.
 """
@@ -54,6 +54,8 @@ def main():
             ("pageable->pageable", b.ctypes.data, a.ctypes.data),
             ("pinned->pinned", pb.data_ptr(), pa.data_ptr()),
             ("host->device", b.ctypes.data, da.data_ptr()),
+            ("pinned->device", pb.data_ptr(), da.data_ptr()),
+            ("device->host", db.data_ptr(), a.ctypes.data),
             ("device->device", db.data_ptr(), da.data_ptr()),
         ]
         reps = args.reps if n <= (1 << 16) else max(20, args.reps // 10)
