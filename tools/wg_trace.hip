@@ -117,6 +117,40 @@ __global__ __launch_bounds__(kThreads) void k_dyn(const char *in, char *io, uint
     }
 }
 
+// the product tile body with U vectors per lane (reduce_tile is U = 4)
+template <int U>
+__device__ __forceinline__ void tile_u(const char *in, char *io, uint64_t base, uint64_t vbytes, uint64_t keepb) {
+    constexpr uint32_t TB = kThreads * U * 16;
+    const uint64_t left = vbytes - base;
+    const int nrec = (int)(left < TB ? left : TB);
+    __amdgpu_buffer_rsrc_t rin = __builtin_amdgcn_make_buffer_rsrc((void *)(in + base), 0, nrec, 0x00020000);
+    __amdgpu_buffer_rsrc_t rio = __builtin_amdgcn_make_buffer_rsrc((void *)(io + base), 0, nrec, 0x00020000);
+    const int t = (int)threadIdx.x;
+    const int wb = (t >> 6) * (U * 1024) + (t & 63) * 16;
+    u32x4 a[U], b[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        a[u] = __builtin_amdgcn_raw_buffer_load_b128(rio, wb + u * 1024, 0, kCachePolicyNT);
+        b[u] = __builtin_amdgcn_raw_buffer_load_b128(rin, wb + u * 1024, 0, kCachePolicyNT);
+        if (u + 1 < U) issue_gap();
+    }
+    const bool keep = keep_tile(base, vbytes, keepb);
+#pragma unroll
+    for (int u = 0; u < U; ++u) store16(combine16<OpSum, float>(a[u], b[u]), rio, wb + u * 1024, keep);
+}
+
+// the last `tail` bytes in smaller tiles (US vectors per lane), dispatched last
+template <int US>
+__global__ __launch_bounds__(kThreads) void k_tailsmall(const char *in, char *io, uint64_t vbytes, uint64_t keep,
+                                                        uint64_t b1, unsigned n1) {
+    if (blockIdx.x < n1) {
+        tile_u<4>(in, io, (uint64_t)blockIdx.x * kTileBytes, vbytes, keep);
+    } else {
+        const uint64_t base = b1 + (uint64_t)(blockIdx.x - n1) * (kThreads * US * 16);
+        if (base < vbytes) tile_u<US>(in, io, base, vbytes, keep);
+    }
+}
+
 static double pct(std::vector<unsigned long long> &v, double p) {
     size_t i = (size_t)(p * (double)(v.size() - 1));
     return (double)v[i];
@@ -155,6 +189,48 @@ int main(int argc, char **argv) {
     printf("fp32 SUM, %zu MiB per operand, %u workgroups x %d threads, %d windows, wall clock %d kHz\n", mib, groups,
            kThreads, nwin, freq_khz);
 
+    if (getenv("WG_TAIL")) {
+        // interleaved A/B of the product kernel and tail-small variants, HIP events
+        struct V { const char *name; int us; int den; };
+        const V vs[] = {{"product", 0, 0}, {"tail 1/16 in 4 KiB", 1, 16}, {"tail 1/8 in 4 KiB", 1, 8},
+                        {"tail 1/16 in 8 KiB", 2, 16}, {"tail 1/32 in 4 KiB", 1, 32}};
+        const int NV = sizeof(vs) / sizeof(vs[0]);
+        std::vector<std::vector<float>> d(NV);
+        for (int it = 0; it < K + 3; ++it) {
+            for (int v = 0; v < NV; ++v) {
+                const size_t off = (size_t)((it * NV + v) % nwin) * bytes;
+                const uint64_t tailb = vs[v].den ? (bytes / vs[v].den) : 0;
+                const uint64_t b1 = bytes - tailb;
+                const unsigned n1 = (unsigned)(b1 / kTileBytes);
+                CK(hipEventRecord(e0, s));
+                if (vs[v].us == 0)
+                    hipLaunchKernelGGL(k_plain, dim3(groups), dim3(kThreads), 0, s, in + off, io + off, (uint64_t)bytes, keep);
+                else {
+                    const unsigned n2 = (unsigned)(tailb / (kThreads * vs[v].us * 16));
+                    if (vs[v].us == 1)
+                        hipLaunchKernelGGL(k_tailsmall<1>, dim3(n1 + n2), dim3(kThreads), 0, s, in + off, io + off,
+                                           (uint64_t)bytes, keep, b1, n1);
+                    else
+                        hipLaunchKernelGGL(k_tailsmall<2>, dim3(n1 + n2), dim3(kThreads), 0, s, in + off, io + off,
+                                           (uint64_t)bytes, keep, b1, n1);
+                }
+                CK(hipEventRecord(e1, s));
+                CK(hipStreamSynchronize(s));
+                float ms = 0;
+                CK(hipEventElapsedTime(&ms, e0, e1));
+                if (it >= 3) d[v].push_back(ms * 1e3f);
+            }
+        }
+        for (int v = 0; v < NV; ++v) {
+            std::sort(d[v].begin(), d[v].end());
+            double mean = 0;
+            for (float x : d[v]) mean += x;
+            mean /= d[v].size();
+            printf("%-22s event mean %7.2f us  median %7.2f  p10 %7.2f  (%.4f of 8 TB/s)\n", vs[v].name, mean,
+                   d[v][d[v].size() / 2], d[v][d[v].size() / 10], 3.0 * bytes / (mean * 1e-6) / 8e12);
+        }
+        return 0;
+    }
     const char *vname[4] = {"plain", "traced", "dyn", "dyn-traced"};
     const int nvar = getenv("WG_DYN") ? 4 : 2;
     const int remap = getenv("WG_REMAP") ? atoi(getenv("WG_REMAP")) : 0;
