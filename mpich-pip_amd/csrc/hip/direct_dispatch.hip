@@ -9,7 +9,9 @@
 // one call's last workgroup and the next call's first.  A direct dispatch
 // waits on the kernel packet's completion signal instead: 7.4-7.5 us, and the
 // 256 MiB fp32 SUM call 126.2-126.4 us against 127.6-127.8 (same box, same
-// kernel).  An earlier attempt (round 1) lost because its kernargs sat in host
+// kernel); with the kernarg cache below and the AQL rings in VRAM
+// (HSA_ALLOCATE_QUEUE_DEV_MEM=1) the gap is 5.2-5.5 us, 4.3 us of it the CP
+// noticing the doorbell (profiles/r02/sync_split_timeline.log, cp_latency.log).  An earlier attempt (round 1) lost because its kernargs sat in host
 // memory (every workgroup read them over PCIe); here they are written through
 // the BAR into VRAM and made visible with an HDP flush (the register ROCr
 // exposes as HSA_AMD_AGENT_INFO_HDP_FLUSH; read back, as HIP does for its
@@ -19,9 +21,11 @@
 //   * synchronous calls on the library's own stream (hip_stream NULL), both
 //     operands on one device, 16 B-aligned with no head / tail elements (the
 //     lean tile kernel), an (op, element) pair the code object carries;
-//   * the legacy null stream is idle (hipStreamQuery(NULL) == hipSuccess, 0.11
-//     us): work the caller queued there for these buffers stays ordered before
-//     the reduction, as with the blocking HIP stream;
+//   * work the caller queued on the legacy null stream for these buffers stays
+//     ordered before the reduction, as with the blocking HIP stream: when
+//     hipStreamQuery(NULL) reports pending work (it keeps doing so for finished
+//     work until the host synchronises, tools/direct_probe.py), the call first
+//     synchronises with the null stream;
 //   * the calling thread has no unfinished work on its own library stream.
 // Packets carry an agent-scope acquire (what HIP uses between kernels; a
 // system-scope acquire costs ~7 us of body, aql_sig_nt_sys) and a
@@ -84,7 +88,8 @@ struct DevState {
     hsa_agent_t agent{};
     hsa_queue_t *queue = nullptr;
     char *karg = nullptr;                       // kKargSlots x kKargSlotBytes, VRAM, host-written
-    std::atomic<uint32_t> kslot{0};
+    uint32_t kslot = 0;                         // next ring slot to try (under `publish`)
+    std::atomic<int> ring_busy[kRingSlots] = {};  // a ring slot's dispatch is in flight
     CacheEntry cache[kCacheSlots];
     volatile uint32_t *hdp = nullptr;
     uint64_t kobj[MPIR_HIP_NOPS][MPIR_HIP_NELEMS] = {};
@@ -402,6 +407,7 @@ int direct_reduce(int dev, int op, int elem, const void *in, void *io, uint64_t 
     const KArgs ka{static_cast<const char *>(in), static_cast<char *>(io), vbytes, keep_for(vbytes)};
     hsa_signal_store_relaxed(sig, 1);
     CacheEntry *held = nullptr;
+    int ring = -1;
     {
         std::lock_guard<std::mutex> lk(d.publish);
         uint64_t h = ko ^ (uint64_t)(uintptr_t)ka.in * 0x9E3779B97F4A7C15ull ^ (uint64_t)(uintptr_t)ka.io * 0xC2B2AE3D27D4EB4Full ^
@@ -420,7 +426,19 @@ int direct_reduce(int dev, int op, int elem, const void *in, void *io, uint64_t 
                 e.args = ka;
             }
         } else {
-            slot = d.karg + (size_t)(d.kslot.fetch_add(1, std::memory_order_relaxed) % kRingSlots) * kKargSlotBytes;
+            // a ring slot no in-flight dispatch reads (workgroups load their
+            // kernargs when they start, i.e. all through a long kernel's life)
+            for (uint32_t k = 0; k < kRingSlots; ++k) {
+                const uint32_t r = (d.kslot + k) % kRingSlots;
+                if (d.ring_busy[r].load(std::memory_order_acquire) == 0) {
+                    ring = (int)r;
+                    break;
+                }
+            }
+            if (ring < 0) return 0;     // every ring slot in flight: the HIP path takes this call
+            d.kslot = (uint32_t)ring + 1;
+            d.ring_busy[ring].store(1, std::memory_order_relaxed);
+            slot = d.karg + (size_t)ring * kKargSlotBytes;
         }
         if (!hit) {
             memcpy(slot, &ka, sizeof ka);
@@ -459,6 +477,7 @@ int direct_reduce(int dev, int op, int elem, const void *in, void *io, uint64_t 
         _mm_pause();
     }
     if (held) held->inflight.fetch_sub(1, std::memory_order_acq_rel);
+    if (ring >= 0) d.ring_busy[ring].store(0, std::memory_order_release);
     if (prof) {
         const uint64_t th2 = sys_ts();
         hsa_amd_profiling_dispatch_time_t t{};

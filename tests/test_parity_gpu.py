@@ -759,6 +759,47 @@ def test_direct_dispatch_path(mpi, orc, cuda):
     assert _direct_count(mpi) == mid
 
 
+def test_direct_dispatch_many_threads_distinct_windows(mpi, cuda):
+    """8 host threads, each rotating over its own 6 windows: the direct
+    dispatch's kernarg cache entries collide across threads and spill to ring
+    slots, which must never be rewritten while a dispatch that reads them is in
+    flight.  Every window's in-place fp32 sums are bit-exact against numpy's
+    float32 sequence of the same additions."""
+    import threading
+    torch = cuda
+    nthreads, nwin, n, iters = 8, 6, (1 << 18) + 16, 30
+    rng = np.random.default_rng(77)
+    a0 = [[rng.uniform(-1, 1, n).astype(np.float32) for _ in range(nwin)] for _ in range(nthreads)]
+    b0 = [[rng.uniform(-1, 1, n).astype(np.float32) for _ in range(nwin)] for _ in range(nthreads)]
+    da = [[torch.from_numpy(x.copy()).cuda() for x in row] for row in a0]
+    db = [[torch.from_numpy(x.copy()).cuda() for x in row] for row in b0]
+    torch.cuda.synchronize()
+    f = mpi.fast_reduce_local()
+    d0 = _direct_count(mpi)
+    errors = []
+
+    def run(k):
+        for i in range(iters):
+            w = (i * 5 + k) % nwin
+            rc = f(db[k][w].data_ptr(), da[k][w].data_ptr(), n, mpi.MPI_FLOAT, mpi.MPI_SUM)
+            if rc:
+                errors.append(rc)
+    th = [threading.Thread(target=run, args=(k,)) for k in range(nthreads)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    assert not errors, errors
+    assert _direct_count(mpi) - d0 >= nthreads * iters // 2      # most calls went direct
+    for k in range(nthreads):
+        want = [x.copy() for x in a0[k]]
+        for i in range(iters):
+            w = (i * 5 + k) % nwin
+            want[w] = want[w] + b0[k][w]
+        for w in range(nwin):
+            assert np.array_equal(da[k][w].cpu().numpy(), want[w]), (k, w)
+
+
 def test_direct_dispatch_orders_after_null_stream(mpi, cuda):
     """Work the caller left running on the legacy null stream for the operands
     is finished before the reduction reads them: the direct path first
