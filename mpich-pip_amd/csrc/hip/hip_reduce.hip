@@ -339,7 +339,7 @@ int get_zc(int dev, size_t bytes, char **out) {
         d.zc = nullptr;
         d.zc_bytes = 0;
         const size_t want = bytes < ((size_t)64 << 10) ? ((size_t)64 << 10) : bytes;
-        HIPCHK(hipHostMalloc(&d.zc, want, hipHostMallocCoherent | hipHostMallocMapped));
+        HIPCHK(hipHostMalloc(&d.zc, want, hipHostMallocCoherent | hipHostMallocMapped | hipHostMallocPortable));
         d.zc_bytes = want;
     }
     *out = d.zc;
