@@ -68,8 +68,9 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1,
                     help="ranks (one per GPU); without WORLD_SIZE in the environment, N > 1 starts N ranks "
                          "itself through torch.distributed.run before any GPU call")
-    ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=50,
+                    help="untimed calls first: the GPU clocks and the kernarg cache settle (profiles/r02/warmup_ab.log)")
     ap.add_argument("--mib", type=int, default=256, help="MiB per operand (metric: 256)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="only the timed MPI_Reduce_local loop")
