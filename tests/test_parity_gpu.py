@@ -718,6 +718,15 @@ def test_mixed_small_path_vs_oracle(mpi, orc, cuda, op, t):
                 run_pair_mixed(mpi, orc, cuda, op, t, n, seed, side, pinned, oh, od)
 
 
+@pytest.mark.parametrize("op,t", MATRIX, ids=[f"{o}-{t}" for o, t in MATRIX])
+def test_mixed_path_matrix_vs_oracle(mpi, orc, cuda, op, t):
+    """Every (op, type) the reference accepts through the mixed-residency path,
+    both directions, a ragged count aligned and a short one misaligned."""
+    for side in ("in", "inout"):
+        run_pair_mixed(mpi, orc, cuda, op, t, 4099, 71, side)
+        run_pair_mixed(mpi, orc, cuda, op, t, 33, 72, side, off_host=5, off_dev=3)
+
+
 def test_mixed_path_crossover(mpi, orc, cuda):
     """Either side of MPIR_Hip_mixed_max_bytes (pinned slot below, staging
     pipeline above), both directions: bit-exact; below it the direct dispatch

@@ -185,6 +185,13 @@ int main(int argc, char **argv) {
     memcpy(g_karg, &ka, sizeof ka);
     HK(hsa_queue_create(g_gpu, 1024, HSA_QUEUE_TYPE_MULTI, nullptr, nullptr, UINT32_MAX, UINT32_MAX, &g_q));
     HK(hsa_amd_profiling_set_profiler_enabled(g_q, 1));
+    if (const char *pr = getenv("QUEUE_PRIORITY")) {
+        const hsa_amd_queue_priority_t qp = !strcmp(pr, "high") ? HSA_AMD_QUEUE_PRIORITY_HIGH
+                                           : !strcmp(pr, "low") ? HSA_AMD_QUEUE_PRIORITY_LOW
+                                                                : HSA_AMD_QUEUE_PRIORITY_NORMAL;
+        HK(hsa_amd_queue_set_priority(g_q, qp));
+        printf("queue priority %s\n", pr);
+    }
     hsa_signal_t s1, s2;
     HK(hsa_signal_create(0, 1, &g_gpu, &s1));
     HK(hsa_signal_create(0, 1, &g_gpu, &s2));
