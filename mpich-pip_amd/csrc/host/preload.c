@@ -26,13 +26,16 @@ typedef int (*reduce_local_fn) (const void *, void *, int, MPI_Datatype, MPI_Op)
 
 static int forward(const void *inbuf, void *inoutbuf, int count, MPI_Datatype datatype, MPI_Op op)
 {
-    static reduce_local_fn next;
+    /* racing first calls resolve the same symbol; the atomics make that well defined */
+    static reduce_local_fn cached;
+    reduce_local_fn next = __atomic_load_n(&cached, __ATOMIC_ACQUIRE);
     if (!next) {
         next = (reduce_local_fn) dlsym(RTLD_NEXT, "PMPI_Reduce_local");
         if (!next) {
             fprintf(stderr, "libmpich_reduce_local_preload: no PMPI_Reduce_local after the shim\n");
             return MPI_ERR_INTERN;
         }
+        __atomic_store_n(&cached, next, __ATOMIC_RELEASE);
     }
     return next(inbuf, inoutbuf, count, datatype, op);
 }
