@@ -465,6 +465,9 @@ int direct_reduce(int dev, int op, int elem, const void *in, void *io, uint64_t 
                                 (release_scope() << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE);
         const uint16_t setup = 1 << HSA_KERNEL_DISPATCH_PACKET_SETUP_DIMENSIONS;
         hsa_queue_store_write_index_relaxed(q, idx + 1);
+        // the ring may be write-combined VRAM (HSA_ALLOCATE_QUEUE_DEV_MEM): the
+        // packet body must be out of the WC buffers before its header is valid
+        _mm_sfence();
         __atomic_store_n((uint32_t *)p, (uint32_t)header | ((uint32_t)setup << 16), __ATOMIC_RELEASE);
         if (prof) th1 = sys_ts();
         hsa_signal_store_screlease(q->doorbell_signal, idx);
