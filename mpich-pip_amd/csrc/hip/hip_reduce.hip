@@ -233,9 +233,9 @@ class CopyPool {
     explicit CopyPool(int nthreads) : n_(nthreads), pid_(getpid()) {
         for (int i = 1; i < n_; ++i) std::thread([this] { work(); }).detach();
     }
-    void copy(char *dst, const char *src, size_t bytes) {
+    void copy(char *dst, const char *src, size_t bytes, size_t min_split = (size_t)1 << 20) {
         // a forked child has none of the workers: copy alone there
-        if (n_ <= 1 || bytes < ((size_t)1 << 20) || getpid() != pid_) {
+        if (n_ <= 1 || bytes < min_split || getpid() != pid_) {
             memcpy(dst, src, bytes);
             return;
         }
@@ -325,6 +325,19 @@ uint64_t mixed_max_bytes() {
         const char *e = getenv("MPIR_CVAR_REDUCE_LOCAL_MIXED_MAX_KB");
         const long kb = e ? atol(e) : 1024;
         return (uint64_t)(kb >= 0 && kb <= (1L << 20) ? kb : 1024) << 10;
+    }();
+    return v;
+}
+
+// copies into / out of the mixed path's slot of at least this many bytes go
+// through the copy pool (MPIR_CVAR_REDUCE_LOCAL_MIXED_SPLIT_KB, default 512: the
+// pool's wake-up costs ~10 us, more than it saves at 256 KiB, less at 1 MiB --
+// device -> host 135 -> 72-85 us; profiles/r02/mixed_split_ab.log)
+size_t zc_split_bytes() {
+    static const size_t v = [] {
+        const char *e = getenv("MPIR_CVAR_REDUCE_LOCAL_MIXED_SPLIT_KB");
+        const long kb = e ? atol(e) : 512;
+        return (size_t)(kb > 0 && kb <= (1L << 20) ? kb : 512) << 10;
     }();
     return v;
 }
@@ -613,13 +626,20 @@ int MPIR_Hip_reduce(const void *inbuf, void *inoutbuf, uint64_t count, int op, i
         int rc = get_zc(dev, (size_t)bytes + 256, &slot);
         if (rc != MPIR_HIP_OK) return rc;
         slot += adev & 255;
+        // host <-> slot copies: split over the copy pool from zc_split_bytes() up
+        auto hcopy = [&](void *dst, const void *src) {
+            if (bytes >= zc_split_bytes())
+                copy_pool().copy(static_cast<char *>(dst), static_cast<const char *>(src), bytes, zc_split_bytes());
+            else
+                memcpy(dst, src, bytes);
+        };
         if (lio == LOC_DEVICE) {
-            memcpy(slot, inbuf, bytes);
+            hcopy(slot, inbuf);
             return device_call(dev, slot, inoutbuf, count, op, elem, nullptr, 1);
         }
-        memcpy(slot, inoutbuf, bytes);
+        hcopy(slot, inoutbuf);
         rc = device_call(dev, inbuf, slot, count, op, elem, nullptr, 1);
-        if (rc == MPIR_HIP_OK) memcpy(inoutbuf, slot, bytes);
+        if (rc == MPIR_HIP_OK) hcopy(inoutbuf, slot);
         return rc;
     }
 
