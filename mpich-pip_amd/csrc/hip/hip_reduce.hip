@@ -233,28 +233,45 @@ class CopyPool {
     explicit CopyPool(int nthreads) : n_(nthreads), pid_(getpid()) {
         for (int i = 1; i < n_; ++i) std::thread([this] { work(); }).detach();
     }
+    int threads() const { return n_; }
+    // fn(ctx, k) for every k < nparts: part 0 on the calling thread, the rest
+    // on the workers; returns when all are done.  One job at a time.
+    void run(size_t nparts, void (*fn)(void *, size_t), void *ctx) {
+        // a forked child has none of the workers: run alone there
+        if (n_ <= 1 || nparts <= 1 || getpid() != pid_) {
+            for (size_t k = 0; k < nparts; ++k) fn(ctx, k);
+            return;
+        }
+        std::lock_guard<std::mutex> job(job_mu_);
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            fn_ = fn;
+            ctx_ = ctx;
+            nparts_ = nparts;
+            next_ = 1;                                  // part 0 is the caller's
+            pending_ = nparts - 1;
+            ++gen_;
+        }
+        cv_.notify_all();
+        fn(ctx, 0);
+        std::unique_lock<std::mutex> lk(mu_);
+        done_.wait(lk, [this] { return pending_ == 0; });
+    }
     void copy(char *dst, const char *src, size_t bytes, size_t min_split = (size_t)1 << 20) {
-        // a forked child has none of the workers: copy alone there
         if (n_ <= 1 || bytes < min_split || getpid() != pid_) {
             memcpy(dst, src, bytes);
             return;
         }
-        std::lock_guard<std::mutex> job(job_mu_);       // one split copy at a time
-        const size_t part = ((bytes + n_ - 1) / n_ + 63) & ~(size_t)63;
-        {
-            std::lock_guard<std::mutex> lk(mu_);
-            dst_ = dst;
-            src_ = src;
-            bytes_ = bytes;
-            part_ = part;
-            next_ = 1;                                  // part 0 is the caller's
-            pending_ = (bytes + part - 1) / part - 1;
-            ++gen_;
-        }
-        cv_.notify_all();
-        memcpy(dst, src, std::min(part, bytes));
-        std::unique_lock<std::mutex> lk(mu_);
-        done_.wait(lk, [this] { return pending_ == 0; });
+        struct C {
+            char *d;
+            const char *s;
+            size_t bytes, part;
+        } c{dst, src, bytes, ((bytes + n_ - 1) / n_ + 63) & ~(size_t)63};
+        run((bytes + c.part - 1) / c.part, [](void *p, size_t k) {
+            const C *c = static_cast<const C *>(p);
+            const size_t o = k * c->part;
+            memcpy(c->d + o, c->s + o, std::min(c->part, c->bytes - o));
+        }, &c);
     }
 
   private:
@@ -264,13 +281,10 @@ class CopyPool {
         for (;;) {
             cv_.wait(lk, [&] { return gen_ != seen; });
             seen = gen_;
-            while (next_ * part_ < bytes_) {
+            while (next_ < nparts_) {
                 const size_t k = next_++;
-                char *d = dst_ + k * part_;
-                const char *sp = src_ + k * part_;
-                const size_t nb = std::min(part_, bytes_ - k * part_);
                 lk.unlock();
-                memcpy(d, sp, nb);
+                fn_(ctx_, k);
                 lk.lock();
                 if (--pending_ == 0) done_.notify_one();
             }
@@ -280,9 +294,9 @@ class CopyPool {
     pid_t pid_;
     std::mutex job_mu_, mu_;
     std::condition_variable cv_, done_;
-    char *dst_ = nullptr;
-    const char *src_ = nullptr;
-    size_t bytes_ = 0, part_ = 1, next_ = 0, pending_ = 0;
+    void (*fn_)(void *, size_t) = nullptr;
+    void *ctx_ = nullptr;
+    size_t nparts_ = 0, next_ = 0, pending_ = 0;
     uint64_t gen_ = 0;
 };
 
@@ -357,6 +371,17 @@ int get_zc(int dev, size_t bytes, char **out) {
     }
     *out = d.zc;
     return MPIR_HIP_OK;
+}
+
+// host combines of at least this many bytes per operand are split over the
+// copy pool's threads (MPIR_CVAR_REDUCE_LOCAL_HOST_SPLIT_KB, default 512)
+uint64_t host_split_bytes() {
+    static const uint64_t v = [] {
+        const char *e = getenv("MPIR_CVAR_REDUCE_LOCAL_HOST_SPLIT_KB");
+        const long kb = e ? atol(e) : 512;
+        return (uint64_t)(kb > 0 && kb <= (1L << 22) ? kb : 512) << 10;
+    }();
+    return v;
 }
 
 // page-locked host memory (hipHostMalloc / hipHostRegister): DMA-able as is
@@ -610,7 +635,26 @@ int MPIR_Hip_reduce(const void *inbuf, void *inoutbuf, uint64_t count, int op, i
     // ---- small, both host-resident: combine on this thread --------------
     if (lin == LOC_HOST && lio == LOC_HOST && count * esz <= host_max_bytes() && g_table[op][elem].host) {
         if (MPIR_Hip_device_count() == 0) return MPIR_HIP_ENODEV;
-        g_table[op][elem].host(inbuf, inoutbuf, count * esz / unit);
+        const uint64_t n = count * esz / unit;
+        if (count * esz < host_split_bytes() || copy_pool().threads() <= 1) {
+            g_table[op][elem].host(inbuf, inoutbuf, n);
+            return MPIR_HIP_OK;
+        }
+        // split over the copy pool's threads, parts on 64-byte boundaries
+        struct H {
+            host_fn fn;
+            const char *in;
+            char *io;
+            uint64_t n, part, unit;
+        } h{g_table[op][elem].host, static_cast<const char *>(inbuf), static_cast<char *>(inoutbuf), n, 0, unit};
+        const uint64_t per = (n + copy_pool().threads() - 1) / copy_pool().threads();
+        const uint64_t grain = unit >= 64 ? 1 : 64 / unit;
+        h.part = (per + grain - 1) / grain * grain;
+        copy_pool().run((size_t)((n + h.part - 1) / h.part), [](void *p, size_t k) {
+            const H *h = static_cast<const H *>(p);
+            const uint64_t b = k * h->part, e = std::min(h->n, b + h->part);
+            h->fn(h->in + b * h->unit, h->io + b * h->unit, e - b);
+        }, &h);
         return MPIR_HIP_OK;
     }
 

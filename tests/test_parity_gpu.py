@@ -651,15 +651,18 @@ def test_host_path_matrix_vs_oracle(mpi, orc, cuda, op, t):
 
 def test_host_path_crossover(mpi, orc, cuda):
     """Either side of MPIR_Hip_host_max_bytes (host combine below, GPU staging
-    above): both bit-exact, for a float and a complex and a pair type."""
+    above), and the host combine split over the copy pool's threads from 512
+    KiB (ragged and misaligned): all bit-exact."""
     lib = mpi.load()
     lib.MPIR_Hip_host_max_bytes.restype = ctypes.c_uint64
     lim = lib.MPIR_Hip_host_max_bytes()
     assert lim == 1 << 20
-    for op, t in (("MPI_SUM", "MPI_FLOAT"), ("MPI_PROD", "MPI_C_DOUBLE_COMPLEX"), ("MPI_MAXLOC", "MPI_DOUBLE_INT")):
+    for op, t in (("MPI_SUM", "MPI_FLOAT"), ("MPI_PROD", "MPI_C_DOUBLE_COMPLEX"), ("MPI_MAXLOC", "MPI_DOUBLE_INT"),
+                  ("MPI_BXOR", "MPI_UNSIGNED_CHAR"), ("MPI_SUM", "MPI_LONG_DOUBLE")):
         esz = T.elem_size(t)
-        for n in (lim // esz, lim // esz + 1):
-            run_pair_host(mpi, orc, op, t, n, 21 + n)
+        # the host combine split over threads (>= 512 KiB), ragged, then either side of the limit
+        for n, off in (((600 << 10) // esz + 3, 0), ((600 << 10) // esz + 1, 3), (lim // esz, 0), (lim // esz + 1, 0)):
+            run_pair_host(mpi, orc, op, t, n, 21 + n, off)
 
 
 def run_pair_mixed(mpi, orc, torch, op, t, n, seed, host_side, pinned=False, off_host=0, off_dev=0):
