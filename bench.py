@@ -33,9 +33,12 @@ Extra fields (rank 0):
                 bytes from the committed rocprofv3 PMC summary (profiles/).
   stream_api    the same combine enqueued back-to-back with MPIX_Reduce_local_stream
                 (the async variant the library's own schedules use).
-  pcie_inclusive  pinned host buffers -> MPI_Reduce_local (H2D + kernel + D2H),
-                the rate when rank buffers arrive in host memory over PiP shm.
-                Reported for DESIGN.md; never `value`.
+  pcie_inclusive  pinned / pageable host buffers -> MPI_Reduce_local forced onto the
+                GPU (host limit 0: H2D + kernel + D2H), the rate when rank buffers
+                arrive in host memory over PiP shm.  Reported for DESIGN.md; never
+                `value`.
+  host_resident the same host buffers under the default dispatch (host combine
+                split over the copy threads, SURVEY §8b "both host -> CPU").
   cpu_baseline  the oracle's C loop (reference algorithm, gcc -O2) on this box's host
                 cores, one pinned thread per physical core (as many as the job's CPU
                 quota allows; every physical core as a secondary, throttled figure),
@@ -571,7 +574,6 @@ def main():
         def hstep(i):
             rc = lib.MPI_Reduce_local(hb.data_ptr(), ha.data_ptr(), count, m.MPI_FLOAT, m.MPI_SUM)
             assert rc == 0
-        dth = time_steps(hstep, hk, 1, sync, barrier, max_over_ranks)
         # pageable host memory (plain malloc'd / shm pages): through the pinned bounce slots
         pa = ha.numpy().copy()
         pb = hb.numpy().copy()
@@ -579,14 +581,32 @@ def main():
         def pstep(i):
             rc = lib.MPI_Reduce_local(pb.ctypes.data, pa.ctypes.data, count, m.MPI_FLOAT, m.MPI_SUM)
             assert rc == 0
-        dtp = time_steps(pstep, hk, 1, sync, barrier, max_over_ranks)
+        # both-host calls take the host combine by default (it beats the PCIe
+        # round trip at every size, profiles/r02/host_crossover.log); the
+        # staging pipeline is forced here with a host limit of 0 so that the
+        # PCIe-inclusive rate of the GPU path stays measured
+        prev = lib.MPIR_Hip_set_host_max_bytes(0)
+        try:
+            dth = time_steps(hstep, hk, 1, sync, barrier, max_over_ranks)
+            dtp = time_steps(pstep, hk, 1, sync, barrier, max_over_ranks)
+        finally:
+            lib.MPIR_Hip_set_host_max_bytes(prev)
         out["pcie_inclusive"] = {"value": round(alg_bytes * hk * world / dth / GIB, 2), "unit": "GiB/s",
                                  "ms_per_step": round(dth / hk * 1e3, 3),
                                  "pageable_value": round(alg_bytes * hk * world / dtp / GIB, 2),
                                  "pageable_ms_per_step": round(dtp / hk * 1e3, 3),
-                                 "note": "host in/inout, 16 MiB chunks through the up (H2D x2) / comp / down (D2H) "
-                                         "stream pipeline; pinned DMA'd directly, pageable via pinned bounce slots "
-                                         "filled and drained by 4 copy threads"}
+                                 "note": "host in/inout forced onto the GPU (host limit 0): 16 MiB chunks through "
+                                         "the up (H2D x2) / comp / down (D2H) stream pipeline; pinned DMA'd directly, "
+                                         "pageable via pinned bounce slots filled and drained by 4 copy threads"}
+        # the default dispatch for the same host buffers: the host combine
+        dhh = time_steps(hstep, hk, 1, sync, barrier, max_over_ranks)
+        dhp = time_steps(pstep, hk, 1, sync, barrier, max_over_ranks)
+        out["host_resident"] = {"value": round(alg_bytes * hk * world / dhh / GIB, 2), "unit": "GiB/s",
+                                "ms_per_step": round(dhh / hk * 1e3, 3),
+                                "pageable_value": round(alg_bytes * hk * world / dhp / GIB, 2),
+                                "pageable_ms_per_step": round(dhp / hk * 1e3, 3),
+                                "note": "same host buffers, default dispatch: combined on the host, split over "
+                                        "the copy threads (SURVEY 8b: both operands host -> CPU)"}
         del ha, hb, pa, pb
 
     if args.collectives == "on" or (args.collectives == "auto" and world > 1 and not args.no_extras):

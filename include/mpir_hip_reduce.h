@@ -96,9 +96,13 @@ int MPIR_Hip_device_count(void);
 /* per-thread contexts (streams, completion word, scratch) created so far; a
    context returns to a pool when its thread exits and is reused, so this stays
    at the peak number of threads calling at once (diagnostic) */
-/* Largest operand (bytes) combined on the calling thread when both operands
- * are host memory (MPIR_CVAR_REDUCE_LOCAL_HOST_MAX_KB, default 1 MiB). */
+/* Largest operand (bytes) combined on the host when both operands are host
+ * memory (MPIR_CVAR_REDUCE_LOCAL_HOST_MAX_KB; default no limit, 0 = always
+ * stage through the GPU).  The setter changes it at run time (an MPI_T-style
+ * cvar write; bench.py uses it to time the staging pipeline) and returns the
+ * previous value. */
 uint64_t MPIR_Hip_host_max_bytes(void);
+uint64_t MPIR_Hip_set_host_max_bytes(uint64_t bytes);
 
 /* One operand host memory, the other on a device, at most this many bytes
  * (MPIR_CVAR_REDUCE_LOCAL_MIXED_MAX_KB, default 1 MiB): the host operand is

@@ -12,6 +12,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <atomic>
 #include <condition_variable>
 #include <mutex>
 #include <thread>
@@ -312,21 +313,23 @@ CopyPool &copy_pool() {
 enum Loc { LOC_HOST = 0, LOC_DEVICE = 1 };
 
 // Both operands in host memory and at most this many bytes each: the combine
-// runs on the calling thread (host_loop, the same functors as the kernels)
-// instead of a staged GPU round trip.  Measured on the MI355X host
-// (tools/host_latency.py, profiles/r02/host_latency_staged.log, host_latency.log), fp32 SUM: a staged
-// call costs 47-50 us up to 16 KiB and 125 us (pinned) / 200 us (pageable) at
-// 1 MiB, the reference's CPU loop 1.8 us at 4 B and 115 us at 1 MiB, 453 us at
-// 4 MiB (GPU: 297 / 505).  MPIR_CVAR_REDUCE_LOCAL_HOST_MAX_KB (default 1024;
-// 0 = always stage through the GPU).
-uint64_t host_max_bytes() {
-    static const uint64_t v = [] {
-        const char *e = getenv("MPIR_CVAR_REDUCE_LOCAL_HOST_MAX_KB");
-        const long kb = e ? atol(e) : 1024;
-        return (uint64_t)(kb >= 0 && kb <= (1L << 22) ? kb : 1024) << 10;
-    }();
-    return v;
-}
+// runs on the host (host_loop, the same functors as the kernels; split over
+// the copy pool's threads from host_split_bytes()) instead of a staged GPU
+// round trip -- SURVEY.md §8b's dispatch rule ("both host -> CPU").  Measured
+// on the MI355X host, fp32 SUM (tools/host_latency.py, tools/host_crossover.py,
+// profiles/r02/host_latency*.log, host_crossover.log): the host combine wins at
+// every size -- 0.4 us against 48 us staged at 4 B, 35 against 125-194 us at
+// 1 MiB, 108 against 299-466 us at 4 MiB, 5.6-5.7 against 10.7-13.9 ms at 256 MiB
+// (staging is PCIe-bound, ~50 GB/s up).  MPIR_CVAR_REDUCE_LOCAL_HOST_MAX_KB:
+// unset or negative = no limit (default), 0 = always stage through the GPU;
+// MPIR_Hip_set_host_max_bytes() changes it at run time (as an MPI_T cvar write).
+std::atomic<uint64_t> g_host_max{[] {
+    const char *e = getenv("MPIR_CVAR_REDUCE_LOCAL_HOST_MAX_KB");
+    if (!e) return ~(uint64_t)0;
+    const long long kb = atoll(e);
+    return kb < 0 ? ~(uint64_t)0 : ((uint64_t)kb << 10);
+}()};
+uint64_t host_max_bytes() { return g_host_max.load(std::memory_order_relaxed); }
 
 // One operand in host memory, the other on a device, at most this many bytes:
 // the host operand is copied into a pinned, device-mapped slot and the kernel
@@ -518,6 +521,8 @@ int MPIR_Hip_has_kernel(int op, int elem) {
 const char *MPIR_Hip_error_string(void) { return ctx().err; }
 
 uint64_t MPIR_Hip_host_max_bytes(void) { return host_max_bytes(); }
+
+uint64_t MPIR_Hip_set_host_max_bytes(uint64_t bytes) { return g_host_max.exchange(bytes); }
 
 uint64_t MPIR_Hip_mixed_max_bytes(void) { return mixed_max_bytes(); }
 

@@ -119,7 +119,7 @@ EXPORTED_SYMBOLS = [
     # the HIP shim (include/mpir_hip_reduce.h)
     "MPIR_Hip_reduce", "MPIR_Hip_elem_size", "MPIR_Hip_has_kernel", "MPIR_Hip_is_device_ptr",
     "MPIR_Hip_memcpy", "MPIR_Hip_error_string", "MPIR_Hip_device_count", "MPIR_Hip_thread_contexts",
-    "MPIR_Hip_host_max_bytes", "MPIR_Hip_mixed_max_bytes", "MPIR_Hip_direct_dispatches", "MPIR_Hip_direct_profile",
+    "MPIR_Hip_host_max_bytes", "MPIR_Hip_set_host_max_bytes", "MPIR_Hip_mixed_max_bytes", "MPIR_Hip_direct_dispatches", "MPIR_Hip_direct_profile",
     "MPIR_Hip_direct_last_kernel_ns", "MPIR_Hip_direct_state", "MPIR_Hip_direct_busy_skips",
     "MPIR_Hip_direct_last_split",
     # runtime subset for config 1 (include/mpi_pip.h)
@@ -190,6 +190,8 @@ def load(path: str | None = None) -> ctypes.CDLL:
     lib.MPIR_Hip_device_count.restype = i32
     lib.MPIR_Hip_thread_contexts.restype = i32
     lib.MPIR_Hip_host_max_bytes.restype = ctypes.c_uint64
+    lib.MPIR_Hip_set_host_max_bytes.argtypes = [ctypes.c_uint64]
+    lib.MPIR_Hip_set_host_max_bytes.restype = ctypes.c_uint64
     lib.MPIR_Hip_mixed_max_bytes.restype = ctypes.c_uint64
     lib.MPIR_Hip_direct_dispatches.restype = ctypes.c_uint64
     lib.MPIR_Hip_direct_profile.argtypes = [i32]

@@ -19,6 +19,24 @@ pytestmark = pytest.mark.gpu
 GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
 
+class host_max:
+    """Set MPIR_Hip_set_host_max_bytes for a block (0 = both-host calls take the
+    GPU staging pipeline instead of the host combine), restoring it after."""
+
+    def __init__(self, mpi, nbytes):
+        self.lib, self.nbytes = mpi.load(), nbytes
+
+    def __enter__(self):
+        self.lib.MPIR_Hip_set_host_max_bytes.restype = ctypes.c_uint64
+        self.lib.MPIR_Hip_set_host_max_bytes.argtypes = [ctypes.c_uint64]
+        self.prev = self.lib.MPIR_Hip_set_host_max_bytes(self.nbytes)
+        return self
+
+    def __exit__(self, *exc):
+        self.lib.MPIR_Hip_set_host_max_bytes(self.prev)
+        return False
+
+
 def dev(torch, host_bytes: np.ndarray, offset: int = 0):
     """Copy bytes to a fresh device allocation at `offset`; returns (tensor, address)."""
     n = host_bytes.size
@@ -164,13 +182,22 @@ def test_survey_probes_on_gpu(mpi, cuda):
         assert [int(x) for x in got] == c["expect"], c["id"]
 
 
+@pytest.mark.parametrize("staged", [False, True], ids=["dispatch", "staged"])
 @pytest.mark.parametrize("where", ["host-host", "host-dev", "dev-host", "pinned-pinned", "pinned-dev",
                                    "host-pinned", "pinned-host", "hostoff-hostoff"])
-def test_host_and_mixed_pointers(mpi, orc, cuda, where):
-    """Rank buffers that arrive in host memory (PiP shm) are staged through the GPU:
+def test_host_and_mixed_pointers(mpi, orc, cuda, where, staged):
+    """Rank buffers that arrive in host memory (PiP shm): with the default
+    dispatch, both-host calls run the host combine and mixed ones the pinned
+    slot (<= 1 MiB) or the staging pipeline; `staged` forces every both-host
+    call through the GPU staging pipeline too (MPIR_Hip_set_host_max_bytes(0)):
     pageable operands through the pinned bounce slots (several chunks per call at
-    the 192 MiB size, so slots are reused), pinned ones DMA'd directly; `hostoff`
-    is a pageable buffer 4 bytes past 64 B alignment."""
+    the 192 MiB size, so slots are reused), pinned ones DMA'd directly.
+    `hostoff` is a pageable buffer 4 bytes past 64 B alignment."""
+    with host_max(mpi, 0 if staged else (1 << 64) - 1):
+        _host_and_mixed_pointers(mpi, orc, cuda, where)
+
+
+def _host_and_mixed_pointers(mpi, orc, cuda, where):
     torch = cuda
     for n, t, op in ((1000, "MPI_FLOAT", "MPI_SUM"), (3 * (16 << 20) + 5, "MPI_INT", "MPI_MAX"),
                      (777, "MPI_DOUBLE_INT", "MPI_MINLOC"), ((9 << 20) + 3, "MPI_DOUBLE", "MPI_SUM")):
@@ -512,11 +539,18 @@ def test_thread_contexts_reused(mpi, cuda):
     assert torch.equal(x, torch.arange(n, dtype=torch.int64, device="cuda") + 65)
 
 
-def test_concurrent_pageable_threads(mpi, orc, cuda):
+@pytest.mark.parametrize("staged", [False, True], ids=["dispatch", "staged"])
+def test_concurrent_pageable_threads(mpi, orc, cuda, staged):
     """Four host threads reduce pageable host buffers at once (the binding
-    releases the GIL around the call): each has its own
-    staging streams and bounce slots, and they share the copy pool (one split
-    copy at a time); every result bit-exact."""
+    releases the GIL around the call).  Staged (MPIR_Hip_set_host_max_bytes(0)):
+    each thread has its own staging streams and bounce slots and they share the
+    copy pool (one split copy at a time); default dispatch: the host combine,
+    split over the same pool.  Every result bit-exact."""
+    with host_max(mpi, 0 if staged else (1 << 64) - 1):
+        _concurrent_pageable_threads(mpi)
+
+
+def _concurrent_pageable_threads(mpi):
     import threading
     n = (10 << 20) + 17                      # 40 MiB of fp32: several 16 MiB chunks per call
     rng = np.random.default_rng(9)
@@ -650,19 +684,23 @@ def test_host_path_matrix_vs_oracle(mpi, orc, cuda, op, t):
 
 
 def test_host_path_crossover(mpi, orc, cuda):
-    """Either side of MPIR_Hip_host_max_bytes (host combine below, GPU staging
-    above), and the host combine split over the copy pool's threads from 512
-    KiB (ragged and misaligned): all bit-exact."""
+    """Either side of a host limit set with MPIR_Hip_set_host_max_bytes (host
+    combine below, GPU staging above; the default is no limit), and the host
+    combine split over the copy pool's threads from 512 KiB (ragged and
+    misaligned): all bit-exact."""
     lib = mpi.load()
     lib.MPIR_Hip_host_max_bytes.restype = ctypes.c_uint64
-    lim = lib.MPIR_Hip_host_max_bytes()
-    assert lim == 1 << 20
-    for op, t in (("MPI_SUM", "MPI_FLOAT"), ("MPI_PROD", "MPI_C_DOUBLE_COMPLEX"), ("MPI_MAXLOC", "MPI_DOUBLE_INT"),
-                  ("MPI_BXOR", "MPI_UNSIGNED_CHAR"), ("MPI_SUM", "MPI_LONG_DOUBLE")):
-        esz = T.elem_size(t)
-        # the host combine split over threads (>= 512 KiB), ragged, then either side of the limit
-        for n, off in (((600 << 10) // esz + 3, 0), ((600 << 10) // esz + 1, 3), (lim // esz, 0), (lim // esz + 1, 0)):
-            run_pair_host(mpi, orc, op, t, n, 21 + n, off)
+    assert lib.MPIR_Hip_host_max_bytes() == (1 << 64) - 1      # default: no limit
+    lim = 1 << 20
+    with host_max(mpi, lim):
+        for op, t in (("MPI_SUM", "MPI_FLOAT"), ("MPI_PROD", "MPI_C_DOUBLE_COMPLEX"),
+                      ("MPI_MAXLOC", "MPI_DOUBLE_INT"), ("MPI_BXOR", "MPI_UNSIGNED_CHAR"),
+                      ("MPI_SUM", "MPI_LONG_DOUBLE")):
+            esz = T.elem_size(t)
+            # the host combine split over threads (>= 512 KiB), ragged, then either side of the limit
+            for n, off in (((600 << 10) // esz + 3, 0), ((600 << 10) // esz + 1, 3), (lim // esz, 0),
+                           (lim // esz + 1, 0)):
+                run_pair_host(mpi, orc, op, t, n, 21 + n, off)
 
 
 def run_pair_mixed(mpi, orc, torch, op, t, n, seed, host_side, pinned=False, off_host=0, off_dev=0):
