@@ -424,15 +424,18 @@ def main():
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world} (launched by an external launcher); "
               f"measuring WORLD_SIZE ranks", file=sys.stderr)
     torch.cuda.set_device(local)
-    if world > 1:
+    # BENCH_TEST_PG=1 (test only): the N > 1 plumbing -- RCCL process group,
+    # barriers, max over ranks -- at WORLD_SIZE 1, to rehearse it on one GPU
+    use_pg = world > 1 or os.environ.get("BENCH_TEST_PG") == "1"
+    if use_pg:
         dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
 
     def barrier():
-        if world > 1:
+        if use_pg:
             dist.barrier()
 
     def max_over_ranks(x: float) -> float:
-        if world == 1:
+        if not use_pg:
             return x
         t = torch.tensor([x], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -618,7 +621,7 @@ def main():
         out["cpu_baseline"] = cpu_baseline(args, count, alg_bytes)
     if rank == 0:
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if use_pg:
         dist.destroy_process_group()
 
 

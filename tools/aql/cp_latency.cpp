@@ -183,7 +183,11 @@ int main(int argc, char **argv) {
     HK(hsa_amd_agents_allow_access(1, &g_gpu, nullptr, g_karg));
     KArgs ka{(const char *)dev, (char *)dev + 32768, 16384, 0};
     memcpy(g_karg, &ka, sizeof ka);
-    HK(hsa_queue_create(g_gpu, 1024, HSA_QUEUE_TYPE_MULTI, nullptr, nullptr, UINT32_MAX, UINT32_MAX, &g_q));
+    // QUEUE_SINGLE=1: a single-producer queue; QUEUE_SIZE: packets in the ring
+    const uint32_t qsize = getenv("QUEUE_SIZE") ? (uint32_t)atoi(getenv("QUEUE_SIZE")) : 1024u;
+    const hsa_queue_type32_t qtype = getenv("QUEUE_SINGLE") ? HSA_QUEUE_TYPE_SINGLE : HSA_QUEUE_TYPE_MULTI;
+    printf("queue %s, %u packets\n", qtype == HSA_QUEUE_TYPE_SINGLE ? "single" : "multi", qsize);
+    HK(hsa_queue_create(g_gpu, qsize, qtype, nullptr, nullptr, UINT32_MAX, UINT32_MAX, &g_q));
     HK(hsa_amd_profiling_set_profiler_enabled(g_q, 1));
     if (const char *pr = getenv("QUEUE_PRIORITY")) {
         const hsa_amd_queue_priority_t qp = !strcmp(pr, "high") ? HSA_AMD_QUEUE_PRIORITY_HIGH
@@ -202,7 +206,7 @@ int main(int argc, char **argv) {
     // idle G
     for (double G : {0.0, 5.0, 20.0, 100.0, 1000.0}) {
         if (spin_only) break;
-        std::vector<double> d2s, s2e, e2h;
+        std::vector<double> d2s, s2e, e2h, tot;
         for (int k = 0; k < K + 10; ++k) {
             spin_us(G);
             hsa_signal_store_relaxed(s1, 1);
@@ -219,9 +223,10 @@ int main(int argc, char **argv) {
             d2s.push_back(us(a - t0));
             s2e.push_back(us(b - a));
             e2h.push_back(us(t1 - b));
+            tot.push_back(us(t1 - t0));
         }
-        printf("idle %7.1f us: doorbell->CP start %5.2f  CP start->end %5.2f  CP end->host sees %5.2f\n", G, med(d2s),
-               med(s2e), med(e2h));
+        printf("idle %7.1f us: doorbell->CP start %5.2f  CP start->end %5.2f  CP end->host sees %5.2f  doorbell->host sees %5.2f\n",
+               G, med(d2s), med(s2e), med(e2h), med(tot));
     }
     // pair
     {
