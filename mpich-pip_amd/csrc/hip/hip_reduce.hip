@@ -236,14 +236,17 @@ class CopyPool {
     }
     int threads() const { return n_; }
     // fn(ctx, k) for every k < nparts: part 0 on the calling thread, the rest
-    // on the workers; returns when all are done.  One job at a time.
+    // on the workers; returns when all are done.  One job at a time: a caller
+    // that finds the workers busy with another thread's job runs its parts
+    // alone rather than waiting, so concurrent callers (other devices, other
+    // host combines) never serialise behind each other.
     void run(size_t nparts, void (*fn)(void *, size_t), void *ctx) {
+        std::unique_lock<std::mutex> job(job_mu_, std::defer_lock);
         // a forked child has none of the workers: run alone there
-        if (n_ <= 1 || nparts <= 1 || getpid() != pid_) {
+        if (n_ <= 1 || nparts <= 1 || getpid() != pid_ || !job.try_lock()) {
             for (size_t k = 0; k < nparts; ++k) fn(ctx, k);
             return;
         }
-        std::lock_guard<std::mutex> job(job_mu_);
         {
             std::lock_guard<std::mutex> lk(mu_);
             fn_ = fn;
