@@ -202,6 +202,44 @@ int main(int argc, char **argv) {
     printf("HSA_ALLOCATE_QUEUE_DEV_MEM=%s\n", getenv("HSA_ALLOCATE_QUEUE_DEV_MEM") ? getenv("HSA_ALLOCATE_QUEUE_DEV_MEM") : "(unset)");
 
     const int K = 300;
+    // PRE_RING=1: only the "ring first, publish later" cases.  The slot's
+    // header is INVALID when the doorbell rings; the host publishes the packet
+    // d us later (the time the call's own validation would take), with or
+    // without ringing again.  A CP that does not wait on an INVALID header
+    // shows up as a timeout (wait() ends the run).
+    if (getenv("PRE_RING")) {
+        for (int again = 0; again < 2; ++again) {
+            for (double d : {0.5, 1.0, 2.0, 3.0, 4.0, 6.0}) {
+                std::vector<double> p2s, tot;
+                for (int k = 0; k < K + 10; ++k) {
+                    hsa_signal_store_relaxed(s1, 1);
+                    const uint64_t idx = hsa_queue_load_write_index_relaxed(g_q);
+                    hsa_kernel_dispatch_packet_t *p =
+                        (hsa_kernel_dispatch_packet_t *)g_q->base_address + (idx & (g_q->size - 1));
+                    __atomic_store_n((uint16_t *)p, (uint16_t)(HSA_PACKET_TYPE_INVALID << HSA_PACKET_HEADER_TYPE),
+                                     __ATOMIC_RELEASE);
+                    hsa_queue_store_write_index_relaxed(g_q, idx + 1);
+                    const uint64_t tr = ts();
+                    hsa_signal_store_screlease(g_q->doorbell_signal, idx);
+                    spin_us(d);
+                    write_dispatch(idx, s1, false);
+                    const uint64_t tp = ts();
+                    write_dispatch(idx, s1, true);
+                    if (again) hsa_signal_store_screlease(g_q->doorbell_signal, idx);
+                    wait(s1);
+                    const uint64_t t1 = ts();
+                    uint64_t a, b;
+                    times(s1, &a, &b);
+                    if (k < 10) continue;
+                    p2s.push_back(us(a - tp));
+                    tot.push_back(us(t1 - tr));
+                }
+                printf("pre-ring%s, publish %.1f us later: publish->CP start %5.2f; first ring->host sees %5.2f\n",
+                       again ? " + ring again" : "", d, med(p2s), med(tot));
+            }
+        }
+        return 0;
+    }
     const bool spin_only = getenv("SPIN_ONLY") != nullptr;
     // idle G
     for (double G : {0.0, 5.0, 20.0, 100.0, 1000.0}) {
