@@ -21,6 +21,7 @@
 
 namespace mpir_hip {
 uint64_t keep_bytes() { return getenv("KEEP_MB") ? strtoull(getenv("KEEP_MB"), 0, 10) << 20 : kKeepBytes; }
+uint64_t keep_for(uint64_t vbytes) { return vbytes <= keep_bytes() ? vbytes : 0; }
 }
 using namespace mpir_hip;
 
@@ -132,7 +133,9 @@ int main(int argc, char **argv) {
     size_t mib = argc > 1 ? strtoull(argv[1], 0, 10) : 32;
     int rounds = argc > 2 ? atoi(argv[2]) : 30;
     size_t bytes = mib << 20;
-    const int P = 8, NS = 2;
+    // NSETS (env, default 2): operand sets rotated; with NSETS x block > 256 MB
+    // no output stays in the Infinity Cache from one use to the next
+    const int P = 8, NS = getenv("NSETS") ? std::max(2, atoi(getenv("NSETS"))) : 2;
     std::vector<char *> ins(P * NS), outs(NS);
     std::vector<uint32_t> h(bytes / 4);
     uint32_t x = 0x5EED;
@@ -163,6 +166,12 @@ int main(int argc, char **argv) {
     };
     else vs = {
         {"CHAIN8 f16 product (U1 T1024)", 2, &launch_combine_p<OpSum, _Float16, 8, false>},
+        // the same bytes through the product's fused kernel with other element work:
+        // u32 BXOR (no floating point) and f32 SUM -- is the 8-stream pattern or the
+        // fp16 chain the limit?
+        {"CHAIN8 u32 BXOR product kernel", 4, &launch_combine_p<OpBxor, uint32_t, 8, false>},
+        {"CHAIN8 f32 SUM product kernel", 4, &launch_combine_p<OpSum, float, 8, false>},
+        {"TREE8 f16 SUM product kernel", 2, &launch_combine_p<OpSum, _Float16, 8, true>},
         {"CHAIN8 f16 U1 T256 gap4", 2, &launch_mx<_Float16, false, 1, 256, 4>},
         {"CHAIN8 f16 U1 T512 gap4", 2, &launch_mx<_Float16, false, 1, 512, 4>},
         {"CHAIN8 f16 U1 T1024 gap0", 2, &launch_mx<_Float16, false, 1, 1024, 0>},
