@@ -19,8 +19,10 @@
 //
 // Scope and ordering (the HIP path is used whenever one does not hold):
 //   * synchronous calls on the library's own stream (hip_stream NULL), both
-//     operands on one device, 16 B-aligned with no head / tail elements (the
-//     lean tile kernel), an (op, element) pair the code object carries;
+//     operands on one device, equally aligned mod 16 (tile_split: the lean
+//     tile kernel when there are no head / tail elements, the full one with
+//     them), an (op, element) pair the code object carries -- every op but
+//     REPLACE on every class but the 32-byte ones;
 //   * work the caller queued on the legacy null stream for these buffers stays
 //     ordered before the reduction, as with the blocking HIP stream: when
 //     hipStreamQuery(NULL) reports pending work (it keeps doing so for finished
@@ -57,7 +59,7 @@ namespace mpir_hip {
 namespace {
 
 constexpr int kMaxDirectDev = 64;
-constexpr uint32_t kKargSlots = 256, kKargSlotBytes = 64;
+constexpr uint32_t kKargSlots = 256, kKargSlotBytes = 128;
 // Kernarg slots 0..kRingSlots-1 are a ring for one-off arguments; the rest are
 // a direct-mapped cache: a call whose (kernel, arguments) match a cached slot
 // dispatches with that slot as it stands -- no BAR write and no HDP flush
@@ -68,16 +70,20 @@ constexpr uint32_t kKargSlots = 256, kKargSlotBytes = 64;
 constexpr uint32_t kRingSlots = 128, kCacheSlots = kKargSlots - kRingSlots;
 constexpr uint32_t kQueueSize = 256;
 
-struct KArgs {          // the tile kernel's four explicit arguments (32 bytes)
+struct KArgs {          // the lean tile kernel's four explicit arguments (32 bytes)
     const char *in;
     char *io;
     uint64_t vbytes;
     uint64_t keep;
 };
+// the full tile kernel takes one TileArgs<T> (80 bytes, the same layout for every T)
+constexpr uint32_t kFullArgBytes = sizeof(TileArgs<char>);
+static_assert(kFullArgBytes == 80 && kFullArgBytes <= kKargSlotBytes, "TileArgs layout");
 
 struct CacheEntry {
     uint64_t ko = 0;
-    KArgs args{};
+    uint32_t n = 0;                             // argument bytes (32 or 80)
+    alignas(8) unsigned char args[kFullArgBytes] = {};
     std::atomic<int> inflight{0};
 };
 
@@ -92,7 +98,8 @@ struct DevState {
     std::atomic<int> ring_busy[kRingSlots] = {};  // a ring slot's dispatch is in flight
     CacheEntry cache[kCacheSlots];
     volatile uint32_t *hdp = nullptr;
-    uint64_t kobj[MPIR_HIP_NOPS][MPIR_HIP_NELEMS] = {};
+    uint64_t kobj[MPIR_HIP_NOPS][MPIR_HIP_NELEMS] = {};     // mpir_tile_* (lean)
+    uint64_t kobjx[MPIR_HIP_NOPS][MPIR_HIP_NELEMS] = {};    // mpir_tilex_* (head / tail)
     std::mutex publish;
     std::atomic<int> queue_error{0};
 };
@@ -229,6 +236,14 @@ const char *op_name(int op) {
     case MPIR_HIP_OP_PROD: return "PROD";
     case MPIR_HIP_OP_MAX: return "MAX";
     case MPIR_HIP_OP_MIN: return "MIN";
+    case MPIR_HIP_OP_LAND: return "LAND";
+    case MPIR_HIP_OP_LOR: return "LOR";
+    case MPIR_HIP_OP_LXOR: return "LXOR";
+    case MPIR_HIP_OP_BAND: return "BAND";
+    case MPIR_HIP_OP_BOR: return "BOR";
+    case MPIR_HIP_OP_BXOR: return "BXOR";
+    case MPIR_HIP_OP_MAXLOC: return "MAXLOC";
+    case MPIR_HIP_OP_MINLOC: return "MINLOC";
     default: return nullptr;
     }
 }
@@ -238,7 +253,8 @@ const char *elem_name(int e) {
     switch (e) {
         N(MPIR_HIP_I8) N(MPIR_HIP_U8) N(MPIR_HIP_I16) N(MPIR_HIP_U16) N(MPIR_HIP_I32) N(MPIR_HIP_U32)
         N(MPIR_HIP_I64) N(MPIR_HIP_U64) N(MPIR_HIP_F16) N(MPIR_HIP_F32) N(MPIR_HIP_F64) N(MPIR_HIP_CF32)
-        N(MPIR_HIP_CF64)
+        N(MPIR_HIP_CF64) N(MPIR_HIP_P2INT) N(MPIR_HIP_PFLOATINT) N(MPIR_HIP_PLONGINT) N(MPIR_HIP_PSHORTINT)
+        N(MPIR_HIP_PDOUBLEINT) N(MPIR_HIP_F80)
     default: return nullptr;
     }
 #undef N
@@ -288,18 +304,23 @@ void init_dev(int dev, DevState &d) {
     for (int op = 1; op < MPIR_HIP_NOPS; ++op) {
         for (int e = 1; e < MPIR_HIP_NELEMS; ++e) {
             if (!op_name(op) || !elem_name(e)) continue;
-            const std::string sym = std::string("mpir_tile_") + op_name(op) + "_" + elem_name(e) + ".kd";
-            hsa_executable_symbol_t s;
-            uint64_t ko = 0;
-            uint32_t kas = 0;
-            if (hsa_executable_get_symbol_by_name(exe, sym.c_str(), &f.gpu, &s) != HSA_STATUS_SUCCESS) continue;
-            if (hsa_executable_symbol_get_info(s, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_OBJECT, &ko) != HSA_STATUS_SUCCESS ||
-                hsa_executable_symbol_get_info(s, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_KERNARG_SEGMENT_SIZE, &kas) !=
-                    HSA_STATUS_SUCCESS ||
-                kas != sizeof(KArgs))
-                continue;
-            d.kobj[op][e] = ko;
-            ++found;
+            // both forms, each with the argument size the host writes
+            for (int full = 0; full < 2; ++full) {
+                const std::string sym =
+                    std::string(full ? "mpir_tilex_" : "mpir_tile_") + op_name(op) + "_" + elem_name(e) + ".kd";
+                hsa_executable_symbol_t s;
+                uint64_t ko = 0;
+                uint32_t kas = 0;
+                if (hsa_executable_get_symbol_by_name(exe, sym.c_str(), &f.gpu, &s) != HSA_STATUS_SUCCESS) continue;
+                if (hsa_executable_symbol_get_info(s, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_OBJECT, &ko) !=
+                        HSA_STATUS_SUCCESS ||
+                    hsa_executable_symbol_get_info(s, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_KERNARG_SEGMENT_SIZE, &kas) !=
+                        HSA_STATUS_SUCCESS ||
+                    kas != (full ? kFullArgBytes : (uint32_t)sizeof(KArgs)))
+                    continue;
+                (full ? d.kobjx : d.kobj)[op][e] = ko;
+                ++found;
+            }
         }
     }
     if (!found) return;
@@ -374,19 +395,23 @@ struct DirectSignals {
 };
 thread_local DirectSignals t_sig;
 
-// 1: dispatched and completed (rc set); 0: not applicable, use the HIP path
-int direct_reduce(int dev, int op, int elem, const void *in, void *io, uint64_t vbytes, int *rc) {
+// 1: dispatched and completed (rc set); 0: not applicable, use the HIP path.
+// `ta` is tile_split's view of the call (padding zeroed by the caller): the
+// lean kernel when it has no head / tail elements, the full one otherwise.
+int direct_reduce(int dev, int op, int elem, const TileArgs<char> &ta, int *rc) {
     if (mode() == 0 || dev < 0 || dev >= kMaxDirectDev || op <= 0 || op >= MPIR_HIP_NOPS || elem <= 0 ||
         elem >= MPIR_HIP_NELEMS)
         return 0;
+    const bool lean = ta.nhead == 0 && ta.ntail == 0;
+    const uint64_t vbytes = ta.vbytes;
     const bool prof = g_profile.load(std::memory_order_relaxed) != 0;
     const uint64_t th0 = prof ? sys_ts() : 0;
     uint64_t th1 = 0;
     DevState &d = g_dev[dev];
     std::call_once(d.once, [&] { init_dev(dev, d); });
     if (!d.ok || d.queue_error.load(std::memory_order_relaxed)) return 0;
-    const uint64_t ko = d.kobj[op][elem];
-    if (!ko || vbytes == 0 || vbytes / 16384 >= (1ull << 26)) return 0;
+    const uint64_t ko = (lean ? d.kobj : d.kobjx)[op][elem];
+    if (!ko || (lean && vbytes == 0) || vbytes / 16384 >= (1ull << 26)) return 0;
     // Work queued on the legacy null stream stays ordered before us, as it is
     // for the HIP path's blocking library stream.  hipStreamQuery(nullptr)
     // keeps answering "not ready" after such work has finished until the host
@@ -403,27 +428,42 @@ int direct_reduce(int dev, int op, int elem, const void *in, void *io, uint64_t 
     }
     hsa_signal_t sig;
     if (!t_sig.get(dev, &sig)) return 0;
-    const uint32_t groups = (uint32_t)((vbytes + kTileBytes - 1) / kTileBytes);
-    const KArgs ka{static_cast<const char *>(in), static_cast<char *>(io), vbytes, keep_for(vbytes)};
+    uint32_t groups = (uint32_t)((vbytes + kTileBytes - 1) / kTileBytes);
+    if (groups == 0) groups = 1;        // head / tail only: workgroup 0 does them
+    alignas(8) unsigned char ka[kFullArgBytes] = {};
+    uint32_t kn;
+    if (lean) {
+        const KArgs k{ta.in, ta.io, ta.vbytes, ta.keep};
+        memcpy(ka, &k, sizeof k);
+        kn = sizeof k;
+    } else {
+        memcpy(ka, &ta, kFullArgBytes);
+        kn = kFullArgBytes;
+    }
     hsa_signal_store_relaxed(sig, 1);
     CacheEntry *held = nullptr;
     int ring = -1;
     {
         std::lock_guard<std::mutex> lk(d.publish);
-        uint64_t h = ko ^ (uint64_t)(uintptr_t)ka.in * 0x9E3779B97F4A7C15ull ^ (uint64_t)(uintptr_t)ka.io * 0xC2B2AE3D27D4EB4Full ^
-                     ka.vbytes * 0x165667B19E3779F9ull ^ ka.keep;
+        uint64_t h = ko;
+        for (uint32_t w = 0; w < kn / 8; ++w) {
+            uint64_t x;
+            memcpy(&x, ka + 8 * w, 8);
+            h = (h ^ x) * 0x9E3779B97F4A7C15ull;
+        }
         h ^= h >> 29;
         const uint32_t ci = (uint32_t)(h % kCacheSlots);
         CacheEntry &e = d.cache[ci];
         char *slot;
-        const bool hit = e.ko == ko && !memcmp(&e.args, &ka, sizeof ka);
+        const bool hit = e.ko == ko && e.n == kn && !memcmp(e.args, ka, kn);
         if (hit || e.inflight.load(std::memory_order_acquire) == 0) {
             slot = d.karg + (size_t)(kRingSlots + ci) * kKargSlotBytes;
             e.inflight.fetch_add(1, std::memory_order_acq_rel);
             held = &e;
             if (!hit) {
                 e.ko = ko;
-                e.args = ka;
+                e.n = kn;
+                memcpy(e.args, ka, kn);
             }
         } else {
             // a ring slot no in-flight dispatch reads (workgroups load their
@@ -441,7 +481,7 @@ int direct_reduce(int dev, int op, int elem, const void *in, void *io, uint64_t 
             slot = d.karg + (size_t)ring * kKargSlotBytes;
         }
         if (!hit) {
-            memcpy(slot, &ka, sizeof ka);
+            memcpy(slot, ka, kn);
             _mm_sfence();
             *d.hdp = 1u;        // HDP flush: the BAR writes land in VRAM before the CP reads them
             (void)*d.hdp;

@@ -26,8 +26,12 @@ typedef hipError_t (*launch_fn)(const void *, void *, uint64_t, hipStream_t);
 typedef hipError_t (*any_fn)(const void *const *, int, int, void *, uint64_t, hipStream_t);
 typedef hipError_t (*multi_fn)(const void *const *, void *, uint64_t, hipStream_t);
 typedef void (*host_fn)(const void *, void *, uint64_t);
+typedef bool (*split_fn)(const void *, void *, uint64_t, void *);
 
-struct Entry { launch_fn fn; any_fn any; host_fn host; };
+// split: tile_split<T> (reduce_kernels.hpp) for the classes whose launcher is
+// the tile family -- the direct AQL dispatch's eligibility test and argument
+// builder; null for the 32-byte classes (LDS transpose) and REPLACE
+struct Entry { launch_fn fn; any_fn any; host_fn host; split_fn split; };
 
 // inout[i] = Op(inout[i], in[i]) on the host, element by element, through the
 // device functors compiled for x86 (unaligned operands: memcpy'd elements)
@@ -51,7 +55,10 @@ template <class Op, class T>
 void reg(int op, int elem) {
     g_table[op][elem].fn = &launch_reduce<Op, T>;
     g_table[op][elem].host = &host_loop<Op, T>;
-    if constexpr (!__is_same(Op, OpReplace)) g_table[op][elem].any = &launch_combine_any<Op, T>;
+    if constexpr (!__is_same(Op, OpReplace)) {
+        g_table[op][elem].any = &launch_combine_any<Op, T>;
+        g_table[op][elem].split = &tile_split_any<T>;
+    }
 }
 template <class Op, class T, int EPL = 2>
 void reg_wide(int op, int elem) {

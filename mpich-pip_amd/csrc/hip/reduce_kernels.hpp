@@ -298,9 +298,46 @@ __global__ __launch_bounds__(kThreads) void k_reduce_elems(const char *in, char 
     }
 }
 
-// Host-side launcher: splits [in, io) x count into head / 16 B vector body /
-// tail when both pointers share their alignment mod 16, else uses the
-// element-granular kernel.  Returns the launch error.
+// The tile kernels' split of [in, io) x count into head elements (to 16 B-align
+// inoutbuf) / a 16 B vector body / tail elements.  False when the two pointers
+// do not share their alignment mod 16 (or are not naturally aligned): then
+// launch_reduce takes the shift or the element kernel.  Also the direct AQL
+// dispatch's eligibility test (g_table[op][elem].split), so both paths split a
+// call the same way.
+template <class T>
+bool tile_split(const void *in_, void *io_, uint64_t count, TileArgs<T> &a) {
+    const char *in = static_cast<const char *>(in_);
+    char *io = static_cast<char *>(io_);
+    const uintptr_t ai = reinterpret_cast<uintptr_t>(in), ao = reinterpret_cast<uintptr_t>(io);
+    const uint64_t nbytes = count * sizeof(T);
+    const bool natural = (ai % alignof(T) == 0) && (ao % alignof(T) == 0);
+    const uint64_t head0 = (16 - (ao & 15)) & 15;
+    if (!(natural && ((ai ^ ao) & 15) == 0 && head0 % sizeof(T) == 0)) return false;
+    const uint64_t head_bytes = head0 < nbytes ? head0 : nbytes;
+    const uint64_t rest = nbytes - head_bytes;
+    const uint64_t vbytes = rest & ~(uint64_t)15;
+    a.in = in + head_bytes;
+    a.io = io + head_bytes;
+    a.vbytes = vbytes;
+    a.head_in = reinterpret_cast<const T *>(in);
+    a.head_io = reinterpret_cast<T *>(io);
+    a.nhead = (uint32_t)(head_bytes / sizeof(T));
+    a.tail_in = reinterpret_cast<const T *>(in + head_bytes + vbytes);
+    a.tail_io = reinterpret_cast<T *>(io + head_bytes + vbytes);
+    a.ntail = (uint32_t)((rest - vbytes) / sizeof(T));
+    a.keep = keep_for(vbytes);
+    return true;
+}
+
+// the same, type-erased: `out` is a TileArgs<T> (whose layout does not depend on T)
+template <class T>
+bool tile_split_any(const void *in, void *io, uint64_t count, void *out) {
+    return tile_split<T>(in, io, count, *static_cast<TileArgs<T> *>(out));
+}
+
+// Host-side launcher: the tile kernels when tile_split applies, else the
+// shift kernel (inoutbuf element-aligned) or the element-granular kernel.
+// Returns the launch error.
 template <class Op, class T>
 hipError_t launch_reduce(const void *in_, void *io_, uint64_t count, hipStream_t s) {
     const char *in = static_cast<const char *>(in_);
@@ -309,28 +346,15 @@ hipError_t launch_reduce(const void *in_, void *io_, uint64_t count, hipStream_t
     const uint64_t nbytes = count * sizeof(T);
     const bool natural = (ai % alignof(T) == 0) && (ao % alignof(T) == 0);
     const uint64_t head0 = (16 - (ao & 15)) & 15;
-    if (natural && ((ai ^ ao) & 15) == 0 && head0 % sizeof(T) == 0) {
-        const uint64_t head_bytes = head0 < nbytes ? head0 : nbytes;
-        const uint64_t rest = nbytes - head_bytes;
-        const uint64_t vbytes = rest & ~(uint64_t)15;
-        TileArgs<T> a;
-        a.in = in + head_bytes;
-        a.io = io + head_bytes;
-        a.vbytes = vbytes;
-        a.head_in = reinterpret_cast<const T *>(in);
-        a.head_io = reinterpret_cast<T *>(io);
-        a.nhead = (uint32_t)(head_bytes / sizeof(T));
-        a.tail_in = reinterpret_cast<const T *>(in + head_bytes + vbytes);
-        a.tail_io = reinterpret_cast<T *>(io + head_bytes + vbytes);
-        a.ntail = (uint32_t)((rest - vbytes) / sizeof(T));
-        a.keep = keep_for(vbytes);
-        uint64_t grid = (vbytes + kTileBytes - 1) / kTileBytes;
+    TileArgs<T> ta;
+    if (tile_split<T>(in_, io_, count, ta)) {
+        uint64_t grid = (ta.vbytes + kTileBytes - 1) / kTileBytes;
         if (grid == 0) grid = 1;
-        if (a.nhead || a.ntail)
-            hipLaunchKernelGGL((k_reduce_tile<Op, T>), dim3((unsigned)grid), dim3(kThreads), 0, s, a);
+        if (ta.nhead || ta.ntail)
+            hipLaunchKernelGGL((k_reduce_tile<Op, T>), dim3((unsigned)grid), dim3(kThreads), 0, s, ta);
         else
-            hipLaunchKernelGGL((k_reduce_tile_lean<Op, T>), dim3((unsigned)grid), dim3(kThreads), 0, s, a.in, a.io,
-                               a.vbytes, a.keep);
+            hipLaunchKernelGGL((k_reduce_tile_lean<Op, T>), dim3((unsigned)grid), dim3(kThreads), 0, s, ta.in, ta.io,
+                               ta.vbytes, ta.keep);
     } else if ((ao % alignof(T) == 0) && head0 % sizeof(T) == 0 && nbytes >= 2 * kTileBytes) {
         // inoutbuf element-aligned, inbuf at any other offset mod 16: the
         // aligned-load + shuffle + funnel tile kernel (small counts stay
