@@ -19,9 +19,9 @@
 //
 // Scope and ordering (the HIP path is used whenever one does not hold):
 //   * synchronous calls on the library's own stream (hip_stream NULL), both
-//     operands on one device, equally aligned mod 16 (tile_split: the lean
-//     tile kernel when there are no head / tail elements, the full one with
-//     them), an (op, element) pair the code object carries -- every op but
+//     operands on one device, any count and alignment: the kernel of
+//     plan_reduce's launch plan (lean / full tile, shift, element-granular),
+//     for every (op, element) pair the code object carries -- every op but
 //     REPLACE on every class but the 32-byte ones;
 //   * work the caller queued on the legacy null stream for these buffers stays
 //     ordered before the reduction, as with the blocking HIP stream: when
@@ -70,20 +70,18 @@ constexpr uint32_t kKargSlots = 256, kKargSlotBytes = 128;
 constexpr uint32_t kRingSlots = 128, kCacheSlots = kKargSlots - kRingSlots;
 constexpr uint32_t kQueueSize = 256;
 
-struct KArgs {          // the lean tile kernel's four explicit arguments (32 bytes)
-    const char *in;
-    char *io;
-    uint64_t vbytes;
-    uint64_t keep;
-};
-// the full tile kernel takes one TileArgs<T> (80 bytes, the same layout for every T)
-constexpr uint32_t kFullArgBytes = sizeof(TileArgs<char>);
-static_assert(kFullArgBytes == 80 && kFullArgBytes <= kKargSlotBytes, "TileArgs layout");
+// a plan's argument bytes (LeanArgs / TileArgs / ShiftArgs / ElemsArgs,
+// reduce_kernels.hpp; their layouts do not depend on the element type)
+constexpr uint32_t kMaxArgBytes = sizeof(ReducePlan::args);
+static_assert(kMaxArgBytes <= kKargSlotBytes, "kernarg slot too small");
+constexpr uint32_t kPlanArgBytes[kPlanKinds] = {sizeof(LeanArgs), sizeof(TileArgs<char>), sizeof(ShiftArgs<char>),
+                                                sizeof(ElemsArgs), sizeof(ElemsArgs)};
+const char *const kPlanPrefix[kPlanKinds] = {"mpir_tile_", "mpir_tilex_", "mpir_tiles_", "mpir_elems_", "mpir_elemsu_"};
 
 struct CacheEntry {
     uint64_t ko = 0;
-    uint32_t n = 0;                             // argument bytes (32 or 80)
-    alignas(8) unsigned char args[kFullArgBytes] = {};
+    uint32_t n = 0;                             // argument bytes
+    alignas(8) unsigned char args[kMaxArgBytes] = {};
     std::atomic<int> inflight{0};
 };
 
@@ -98,8 +96,7 @@ struct DevState {
     std::atomic<int> ring_busy[kRingSlots] = {};  // a ring slot's dispatch is in flight
     CacheEntry cache[kCacheSlots];
     volatile uint32_t *hdp = nullptr;
-    uint64_t kobj[MPIR_HIP_NOPS][MPIR_HIP_NELEMS] = {};     // mpir_tile_* (lean)
-    uint64_t kobjx[MPIR_HIP_NOPS][MPIR_HIP_NELEMS] = {};    // mpir_tilex_* (head / tail)
+    uint64_t kobj[kPlanKinds][MPIR_HIP_NOPS][MPIR_HIP_NELEMS] = {};   // by plan kind (kPlanPrefix)
     std::mutex publish;
     std::atomic<int> queue_error{0};
 };
@@ -304,10 +301,9 @@ void init_dev(int dev, DevState &d) {
     for (int op = 1; op < MPIR_HIP_NOPS; ++op) {
         for (int e = 1; e < MPIR_HIP_NELEMS; ++e) {
             if (!op_name(op) || !elem_name(e)) continue;
-            // both forms, each with the argument size the host writes
-            for (int full = 0; full < 2; ++full) {
-                const std::string sym =
-                    std::string(full ? "mpir_tilex_" : "mpir_tile_") + op_name(op) + "_" + elem_name(e) + ".kd";
+            // every plan kind, each with the argument size the host writes
+            for (int kind = 0; kind < kPlanKinds; ++kind) {
+                const std::string sym = std::string(kPlanPrefix[kind]) + op_name(op) + "_" + elem_name(e) + ".kd";
                 hsa_executable_symbol_t s;
                 uint64_t ko = 0;
                 uint32_t kas = 0;
@@ -316,9 +312,9 @@ void init_dev(int dev, DevState &d) {
                         HSA_STATUS_SUCCESS ||
                     hsa_executable_symbol_get_info(s, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_KERNARG_SEGMENT_SIZE, &kas) !=
                         HSA_STATUS_SUCCESS ||
-                    kas != (full ? kFullArgBytes : (uint32_t)sizeof(KArgs)))
+                    kas != kPlanArgBytes[kind])
                     continue;
-                (full ? d.kobjx : d.kobj)[op][e] = ko;
+                d.kobj[kind][op][e] = ko;
                 ++found;
             }
         }
@@ -396,22 +392,20 @@ struct DirectSignals {
 thread_local DirectSignals t_sig;
 
 // 1: dispatched and completed (rc set); 0: not applicable, use the HIP path.
-// `ta` is tile_split's view of the call (padding zeroed by the caller): the
-// lean kernel when it has no head / tail elements, the full one otherwise.
-int direct_reduce(int dev, int op, int elem, const TileArgs<char> &ta, int *rc) {
+// `p` is plan_reduce's launch plan of the call (padding bytes zero).
+int direct_reduce(int dev, int op, int elem, const ReducePlan &p, int *rc) {
     if (mode() == 0 || dev < 0 || dev >= kMaxDirectDev || op <= 0 || op >= MPIR_HIP_NOPS || elem <= 0 ||
-        elem >= MPIR_HIP_NELEMS)
+        elem >= MPIR_HIP_NELEMS || p.kind < 0 || p.kind >= kPlanKinds || p.arg_bytes != kPlanArgBytes[p.kind])
         return 0;
-    const bool lean = ta.nhead == 0 && ta.ntail == 0;
-    const uint64_t vbytes = ta.vbytes;
     const bool prof = g_profile.load(std::memory_order_relaxed) != 0;
     const uint64_t th0 = prof ? sys_ts() : 0;
     uint64_t th1 = 0;
     DevState &d = g_dev[dev];
     std::call_once(d.once, [&] { init_dev(dev, d); });
     if (!d.ok || d.queue_error.load(std::memory_order_relaxed)) return 0;
-    const uint64_t ko = (lean ? d.kobj : d.kobjx)[op][elem];
-    if (!ko || (lean && vbytes == 0) || vbytes / 16384 >= (1ull << 26)) return 0;
+    const uint64_t ko = d.kobj[p.kind][op][elem];
+    // the packet's grid_size_x (workgroups x kThreads) is 32 bits
+    if (!ko || p.groups == 0 || p.groups > (uint64_t)UINT32_MAX / kThreads) return 0;
     // Work queued on the legacy null stream stays ordered before us, as it is
     // for the HIP path's blocking library stream.  hipStreamQuery(nullptr)
     // keeps answering "not ready" after such work has finished until the host
@@ -428,18 +422,9 @@ int direct_reduce(int dev, int op, int elem, const TileArgs<char> &ta, int *rc) 
     }
     hsa_signal_t sig;
     if (!t_sig.get(dev, &sig)) return 0;
-    uint32_t groups = (uint32_t)((vbytes + kTileBytes - 1) / kTileBytes);
-    if (groups == 0) groups = 1;        // head / tail only: workgroup 0 does them
-    alignas(8) unsigned char ka[kFullArgBytes] = {};
-    uint32_t kn;
-    if (lean) {
-        const KArgs k{ta.in, ta.io, ta.vbytes, ta.keep};
-        memcpy(ka, &k, sizeof k);
-        kn = sizeof k;
-    } else {
-        memcpy(ka, &ta, kFullArgBytes);
-        kn = kFullArgBytes;
-    }
+    const uint32_t groups = (uint32_t)p.groups;
+    const unsigned char *ka = p.args;
+    const uint32_t kn = p.arg_bytes;
     hsa_signal_store_relaxed(sig, 1);
     CacheEntry *held = nullptr;
     int ring = -1;

@@ -1,19 +1,21 @@
 // direct_tiles.hip -- device-only code object lib/libmpir_hip_tiles.hsaco for
 // the direct AQL dispatch of synchronous calls (direct_dispatch.hip).
 //
-// Two extern "C" kernels per (op, element class) whose launcher is the tile
-// family (reg<Op, T> in the reg_*.hip units: every op on the integer, real,
-// complex, pair and x87 classes except the 32-byte ones and REPLACE), under
-// plain names the host looks up:
-//   mpir_tile_<op>_<element enum>   the body of k_reduce_tile_lean<Op, T>:
-//                                   four arguments (in, io, vbytes, keep), for
-//                                   16 B-aligned operands of 16 B multiples;
-//   mpir_tilex_<op>_<element enum>  the body of k_reduce_tile<Op, T>: one
-//                                   TileArgs<T> (80 bytes), the head / tail
-//                                   elements of a ragged or 16 B-misaligned
-//                                   (but equally misaligned) call combined by
-//                                   workgroup 0.
-// Neither reads a hidden argument (no gridDim), so a bare AQL packet launches it.
+// Five extern "C" kernels per (op, element class) whose launcher is
+// launch_reduce (reg<Op, T> in the reg_*.hip units: every op on the integer,
+// real, complex, pair and x87 classes; not the 32-byte classes or REPLACE) --
+// one per kind of plan_reduce's launch plan (reduce_kernels.hpp), under plain
+// names the host looks up:
+//   mpir_tile_<op>_<elem>    k_reduce_tile_lean's body (LeanArgs, 32 B):
+//                            16 B-aligned operands of 16 B multiples;
+//   mpir_tilex_<op>_<elem>   k_reduce_tile's body (TileArgs, 80 B): equal
+//                            alignment mod 16, head / tail elements by
+//                            workgroup 0;
+//   mpir_tiles_<op>_<elem>   k_reduce_shift's body (ShiftArgs, 96 B): unequal
+//                            alignment mod 16, two tiles or more;
+//   mpir_elems_<op>_<elem>   k_reduce_elems<NATURAL = true / false> (ElemsArgs,
+//   mpir_elemsu_<op>_<elem>  32 B, the grid stride an argument): the rest.
+// None reads a hidden argument (no gridDim), so a bare AQL packet launches it.
 #include "kernel_table.hpp"
 
 using namespace mpir_hip;
@@ -27,6 +29,17 @@ using namespace mpir_hip;
     }                                                                                                     \
     extern "C" __global__ __launch_bounds__(kThreads) void mpir_tilex_##OPN##_##E(TileArgs<T> a) {       \
         reduce_tile_body<OP, T>(a);                                                                       \
+    }                                                                                                     \
+    extern "C" __global__ __launch_bounds__(kThreads) void mpir_tiles_##OPN##_##E(ShiftArgs<T> a) {      \
+        reduce_shift_body<OP, T>(a);                                                                      \
+    }                                                                                                     \
+    extern "C" __global__ __launch_bounds__(kThreads) void mpir_elems_##OPN##_##E(                       \
+        const char *in, char *io, uint64_t n, uint64_t stride) {                                          \
+        reduce_elems<OP, T, true>(in, io, n, stride);                                                     \
+    }                                                                                                     \
+    extern "C" __global__ __launch_bounds__(kThreads) void mpir_elemsu_##OPN##_##E(                      \
+        const char *in, char *io, uint64_t n, uint64_t stride) {                                          \
+        reduce_elems<OP, T, false>(in, io, n, stride);                                                    \
     }
 
 // the (op, class) matrix of reg_sum_prod / reg_max_min / reg_logic / reg_pairs_x87

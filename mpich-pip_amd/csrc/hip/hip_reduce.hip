@@ -29,7 +29,7 @@ namespace {
 }  // namespace
 
 namespace mpir_hip {
-int direct_reduce(int dev, int op, int elem, const TileArgs<char> &ta, int *rc);  // direct_dispatch.hip
+int direct_reduce(int dev, int op, int elem, const ReducePlan &p, int *rc);  // direct_dispatch.hip
 uint64_t direct_calls();
 void direct_profile(int on);
 uint64_t direct_last_kernel_ns();
@@ -467,11 +467,11 @@ int wait_stream(int dev, hipStream_t s) {
 }
 
 // Both operands reachable by device `dev`'s kernels (device memory, or the
-// pinned slot of the mixed path): direct AQL dispatch for a synchronous call
-// on the library stream whenever the tile kernels apply (tile_split: operands
-// equally aligned mod 16, any count) and nothing queued on the library stream
-// is still pending; otherwise -- REPLACE, the 32-byte classes, unequally
-// aligned operands -- the HIP launch (then the wait, for a synchronous call).
+// pinned slot of the mixed path): direct AQL dispatch of plan_reduce's kernel
+// for a synchronous call on the library stream (any count, any alignment) when
+// nothing queued on the library stream is still pending; otherwise -- REPLACE,
+// the 32-byte classes, the stream variant -- the HIP launch (then the wait,
+// for a synchronous call).
 int device_call(int dev, const void *inbuf, void *inoutbuf, uint64_t count, int op, int elem, hipStream_t user_s,
                 int sync) {
     launch_fn fn = g_table[op][elem].fn;
@@ -484,16 +484,16 @@ int device_call(int dev, const void *inbuf, void *inoutbuf, uint64_t count, int 
     hipStream_t s = user_s;
     int rc = MPIR_HIP_OK;
     DevCtx &d = ctx().dev[dev];
-    TileArgs<char> ta;
-    memset(&ta, 0, sizeof ta);      // zero padding: the kernarg cache compares bytes
-    if (sync && !s && g_table[op][elem].split && g_table[op][elem].split(inbuf, inoutbuf, count, &ta)) {
+    if (sync && !s && g_table[op][elem].plan) {
+        ReducePlan plan;
+        g_table[op][elem].plan(inbuf, inoutbuf, count, &plan);
         bool idle = !d.main_pending;
         if (!idle && d.stream[S_MAIN] && hipStreamQuery(d.stream[S_MAIN]) == hipSuccess) {
             d.main_pending = false;
             idle = true;
         }
         (void)hipGetLastError();
-        if (idle && direct_reduce(dev, op, elem, ta, &rc)) {
+        if (idle && direct_reduce(dev, op, elem, plan, &rc)) {
             if (rc != MPIR_HIP_OK) snprintf(ctx().err, sizeof(ctx().err), "direct dispatch: queue error");
             if (cur != dev) (void)hipSetDevice(cur);
             return rc;

@@ -26,12 +26,13 @@ typedef hipError_t (*launch_fn)(const void *, void *, uint64_t, hipStream_t);
 typedef hipError_t (*any_fn)(const void *const *, int, int, void *, uint64_t, hipStream_t);
 typedef hipError_t (*multi_fn)(const void *const *, void *, uint64_t, hipStream_t);
 typedef void (*host_fn)(const void *, void *, uint64_t);
-typedef bool (*split_fn)(const void *, void *, uint64_t, void *);
+typedef void (*plan_fn)(const void *, void *, uint64_t, ReducePlan *);
 
-// split: tile_split<T> (reduce_kernels.hpp) for the classes whose launcher is
-// the tile family -- the direct AQL dispatch's eligibility test and argument
-// builder; null for the 32-byte classes (LDS transpose) and REPLACE
-struct Entry { launch_fn fn; any_fn any; host_fn host; split_fn split; };
+// plan: plan_reduce<T> (reduce_kernels.hpp) for the classes whose launcher is
+// launch_reduce -- the kernel, grid and argument bytes the direct AQL dispatch
+// launches from its code object; null for the 32-byte classes (LDS transpose)
+// and REPLACE (a byte copy), which take the HIP launch
+struct Entry { launch_fn fn; any_fn any; host_fn host; plan_fn plan; };
 
 // inout[i] = Op(inout[i], in[i]) on the host, element by element, through the
 // device functors compiled for x86 (unaligned operands: memcpy'd elements)
@@ -57,7 +58,7 @@ void reg(int op, int elem) {
     g_table[op][elem].host = &host_loop<Op, T>;
     if constexpr (!__is_same(Op, OpReplace)) {
         g_table[op][elem].any = &launch_combine_any<Op, T>;
-        g_table[op][elem].split = &tile_split_any<T>;
+        g_table[op][elem].plan = &plan_reduce_any<T>;
     }
 }
 template <class Op, class T, int EPL = 2>

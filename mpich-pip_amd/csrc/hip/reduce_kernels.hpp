@@ -218,7 +218,7 @@ struct ShiftArgs {
 };
 
 template <class Op, class T>
-__global__ __launch_bounds__(kThreads) void k_reduce_shift(ShiftArgs<T> args) {
+__device__ __forceinline__ void reduce_shift_body(const ShiftArgs<T> &args) {
     const TileArgs<T> &ta = args.t;
     const uint64_t base = (uint64_t)blockIdx.x * kTileBytes;
     if (base < ta.vbytes) {
@@ -276,13 +276,19 @@ __global__ __launch_bounds__(kThreads) void k_reduce_shift(ShiftArgs<T> args) {
     }
 }
 
+template <class Op, class T>
+__global__ __launch_bounds__(kThreads) void k_reduce_shift(ShiftArgs<T> args) {
+    reduce_shift_body<Op, T>(args);
+}
+
 // General path: inbuf and inoutbuf differ in alignment mod 16 (sub-range
 // displacements of arbitrary element counts), or elements are not even
-// naturally aligned.  Element-granular, coalesced, grid-stride.
+// naturally aligned.  Element-granular, coalesced, grid-stride; the stride
+// (grid x kThreads) is an argument, not gridDim, so the direct AQL dispatch
+// can launch it without hidden arguments.
 template <class Op, class T, bool NATURAL>
-__global__ __launch_bounds__(kThreads) void k_reduce_elems(const char *in, char *io, uint64_t n) {
+__device__ __forceinline__ void reduce_elems(const char *in, char *io, uint64_t n, uint64_t stride) {
     Op op;
-    const uint64_t stride = (uint64_t)gridDim.x * kThreads;
     for (uint64_t i = (uint64_t)blockIdx.x * kThreads + threadIdx.x; i < n; i += stride) {
         if constexpr (NATURAL) {
             const T *pi = reinterpret_cast<const T *>(in) + i;
@@ -298,12 +304,14 @@ __global__ __launch_bounds__(kThreads) void k_reduce_elems(const char *in, char 
     }
 }
 
+template <class Op, class T, bool NATURAL>
+__global__ __launch_bounds__(kThreads) void k_reduce_elems(const char *in, char *io, uint64_t n, uint64_t stride) {
+    reduce_elems<Op, T, NATURAL>(in, io, n, stride);
+}
+
 // The tile kernels' split of [in, io) x count into head elements (to 16 B-align
 // inoutbuf) / a 16 B vector body / tail elements.  False when the two pointers
-// do not share their alignment mod 16 (or are not naturally aligned): then
-// launch_reduce takes the shift or the element kernel.  Also the direct AQL
-// dispatch's eligibility test (g_table[op][elem].split), so both paths split a
-// call the same way.
+// do not share their alignment mod 16 (or are not naturally aligned).
 template <class T>
 bool tile_split(const void *in_, void *io_, uint64_t count, TileArgs<T> &a) {
     const char *in = static_cast<const char *>(in_);
@@ -329,17 +337,31 @@ bool tile_split(const void *in_, void *io_, uint64_t count, TileArgs<T> &a) {
     return true;
 }
 
-// the same, type-erased: `out` is a TileArgs<T> (whose layout does not depend on T)
-template <class T>
-bool tile_split_any(const void *in, void *io, uint64_t count, void *out) {
-    return tile_split<T>(in, io, count, *static_cast<TileArgs<T> *>(out));
-}
+// The launch plan of one single-operand reduction: which kernel, its grid and
+// its argument bytes.  launch_reduce launches it through HIP; the direct AQL
+// dispatch (direct_dispatch.hip) launches the same kernel body from its code
+// object -- so both paths treat every call identically.
+enum : int {
+    kPlanLean = 0,      // k_reduce_tile_lean: 16 B-aligned, 16 B multiple (LeanArgs)
+    kPlanFull = 1,      // k_reduce_tile: equal alignment mod 16, head / tail elements (TileArgs)
+    kPlanShift = 2,     // k_reduce_shift: unequal alignment, >= 2 tiles (ShiftArgs)
+    kPlanElems = 3,     // k_reduce_elems<NATURAL = true> (ElemsArgs)
+    kPlanElemsU = 4,    // k_reduce_elems<NATURAL = false> (ElemsArgs)
+    kPlanKinds = 5
+};
+struct LeanArgs { const char *in; char *io; uint64_t vbytes; uint64_t keep; };
+struct ElemsArgs { const char *in; char *io; uint64_t n; uint64_t stride; };
+struct ReducePlan {
+    int kind;
+    uint32_t arg_bytes;
+    uint64_t groups;    // workgroups of kThreads
+    alignas(16) unsigned char args[sizeof(ShiftArgs<char>)];
+};
 
-// Host-side launcher: the tile kernels when tile_split applies, else the
-// shift kernel (inoutbuf element-aligned) or the element-granular kernel.
-// Returns the launch error.
-template <class Op, class T>
-hipError_t launch_reduce(const void *in_, void *io_, uint64_t count, hipStream_t s) {
+// Fills `p` (padding bytes zero: the direct path's kernarg cache compares bytes).
+template <class T>
+void plan_reduce(const void *in_, void *io_, uint64_t count, ReducePlan &p) {
+    __builtin_memset(&p, 0, sizeof p);
     const char *in = static_cast<const char *>(in_);
     char *io = static_cast<char *>(io_);
     const uintptr_t ai = reinterpret_cast<uintptr_t>(in), ao = reinterpret_cast<uintptr_t>(io);
@@ -347,14 +369,20 @@ hipError_t launch_reduce(const void *in_, void *io_, uint64_t count, hipStream_t
     const bool natural = (ai % alignof(T) == 0) && (ao % alignof(T) == 0);
     const uint64_t head0 = (16 - (ao & 15)) & 15;
     TileArgs<T> ta;
+    __builtin_memset(&ta, 0, sizeof ta);
     if (tile_split<T>(in_, io_, count, ta)) {
-        uint64_t grid = (ta.vbytes + kTileBytes - 1) / kTileBytes;
-        if (grid == 0) grid = 1;
-        if (ta.nhead || ta.ntail)
-            hipLaunchKernelGGL((k_reduce_tile<Op, T>), dim3((unsigned)grid), dim3(kThreads), 0, s, ta);
-        else
-            hipLaunchKernelGGL((k_reduce_tile_lean<Op, T>), dim3((unsigned)grid), dim3(kThreads), 0, s, ta.in, ta.io,
-                               ta.vbytes, ta.keep);
+        p.groups = (ta.vbytes + kTileBytes - 1) / kTileBytes;
+        if (p.groups == 0) p.groups = 1;
+        if (ta.nhead || ta.ntail) {
+            p.kind = kPlanFull;
+            __builtin_memcpy(p.args, &ta, sizeof ta);
+            p.arg_bytes = sizeof ta;
+        } else {
+            const LeanArgs la{ta.in, ta.io, ta.vbytes, ta.keep};
+            p.kind = kPlanLean;
+            __builtin_memcpy(p.args, &la, sizeof la);
+            p.arg_bytes = sizeof la;
+        }
     } else if ((ao % alignof(T) == 0) && head0 % sizeof(T) == 0 && nbytes >= 2 * kTileBytes) {
         // inoutbuf element-aligned, inbuf at any other offset mod 16: the
         // aligned-load + shuffle + funnel tile kernel (small counts stay
@@ -363,6 +391,7 @@ hipError_t launch_reduce(const void *in_, void *io_, uint64_t count, hipStream_t
         const uint64_t rest = nbytes - head_bytes;
         const uint64_t vbytes = rest & ~(uint64_t)15;
         ShiftArgs<T> a;
+        __builtin_memset(&a, 0, sizeof a);
         a.t.in = nullptr;
         a.t.io = io + head_bytes;
         a.t.vbytes = vbytes;
@@ -376,16 +405,62 @@ hipError_t launch_reduce(const void *in_, void *io_, uint64_t count, hipStream_t
         const uintptr_t vin = ai + head_bytes;
         a.delta = (uint32_t)(vin & 15);
         a.in_al = reinterpret_cast<const char *>(vin - a.delta);
-        uint64_t grid = (vbytes + kTileBytes - 1) / kTileBytes;
-        hipLaunchKernelGGL((k_reduce_shift<Op, T>), dim3((unsigned)grid), dim3(kThreads), 0, s, a);
+        p.kind = kPlanShift;
+        p.groups = (vbytes + kTileBytes - 1) / kTileBytes;
+        __builtin_memcpy(p.args, &a, sizeof a);
+        p.arg_bytes = sizeof a;
     } else {
         uint64_t grid = (count + kThreads - 1) / kThreads;
         if (grid > 4096) grid = 4096;
         if (grid == 0) grid = 1;
-        if (natural)
-            hipLaunchKernelGGL((k_reduce_elems<Op, T, true>), dim3((unsigned)grid), dim3(kThreads), 0, s, in, io, count);
+        const ElemsArgs ea{in, io, count, grid * kThreads};
+        p.kind = natural ? kPlanElems : kPlanElemsU;
+        p.groups = grid;
+        __builtin_memcpy(p.args, &ea, sizeof ea);
+        p.arg_bytes = sizeof ea;
+    }
+}
+
+// the same, type-erased (Entry::plan, kernel_table.hpp)
+template <class T>
+void plan_reduce_any(const void *in, void *io, uint64_t count, ReducePlan *p) {
+    plan_reduce<T>(in, io, count, *p);
+}
+
+// Host-side launcher: the plan's kernel through HIP.  Returns the launch error.
+template <class Op, class T>
+hipError_t launch_reduce(const void *in, void *io, uint64_t count, hipStream_t s) {
+    ReducePlan p;
+    plan_reduce<T>(in, io, count, p);
+    const dim3 grid((unsigned)p.groups), block(kThreads);
+    switch (p.kind) {
+    case kPlanLean: {
+        LeanArgs a;
+        __builtin_memcpy(&a, p.args, sizeof a);
+        hipLaunchKernelGGL((k_reduce_tile_lean<Op, T>), grid, block, 0, s, a.in, a.io, a.vbytes, a.keep);
+        break;
+    }
+    case kPlanFull: {
+        TileArgs<T> a;
+        __builtin_memcpy(&a, p.args, sizeof a);
+        hipLaunchKernelGGL((k_reduce_tile<Op, T>), grid, block, 0, s, a);
+        break;
+    }
+    case kPlanShift: {
+        ShiftArgs<T> a;
+        __builtin_memcpy(&a, p.args, sizeof a);
+        hipLaunchKernelGGL((k_reduce_shift<Op, T>), grid, block, 0, s, a);
+        break;
+    }
+    default: {
+        ElemsArgs a;
+        __builtin_memcpy(&a, p.args, sizeof a);
+        if (p.kind == kPlanElems)
+            hipLaunchKernelGGL((k_reduce_elems<Op, T, true>), grid, block, 0, s, a.in, a.io, a.n, a.stride);
         else
-            hipLaunchKernelGGL((k_reduce_elems<Op, T, false>), dim3((unsigned)grid), dim3(kThreads), 0, s, in, io, count);
+            hipLaunchKernelGGL((k_reduce_elems<Op, T, false>), grid, block, 0, s, a.in, a.io, a.n, a.stride);
+        break;
+    }
     }
     return hipGetLastError();
 }
@@ -466,7 +541,8 @@ hipError_t launch_reduce_wide(const void *in_, void *io_, uint64_t count, hipStr
     uint64_t grid = (count + kThreads - 1) / kThreads;
     if (grid > 4096) grid = 4096;
     if (grid == 0) grid = 1;
-    hipLaunchKernelGGL((k_reduce_elems<Op, T, false>), dim3((unsigned)grid), dim3(kThreads), 0, s, in, io, count);
+    hipLaunchKernelGGL((k_reduce_elems<Op, T, false>), dim3((unsigned)grid), dim3(kThreads), 0, s, in, io, count,
+                       grid * kThreads);
     return hipGetLastError();
 }
 

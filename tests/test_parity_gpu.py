@@ -794,12 +794,12 @@ def _direct_count(mpi):
 
 
 def test_direct_dispatch_path(mpi, orc, cuda):
-    """Synchronous device-resident calls whose operands share their alignment
-    mod 16 go through the direct AQL dispatch (direct_dispatch.hip): the lean
-    tile kernel for 16 B-aligned 16 B multiples, the full one (head / tail
-    elements by workgroup 0) for ragged counts and equal misalignment, every op
-    but REPLACE.  Unequally aligned operands, and the 32-byte classes, take the
-    HIP launch.  Every result bit-exact against the oracle."""
+    """Synchronous device-resident calls go through the direct AQL dispatch
+    (direct_dispatch.hip) with the kernel of plan_reduce's launch plan: the
+    lean tile kernel (16 B-aligned 16 B multiples), the full one (head / tail
+    elements), the shift kernel (unequal alignment mod 16) and the element
+    kernels (small unequal or unnatural alignment), for every op but REPLACE;
+    the 32-byte classes take the HIP launch.  Every result bit-exact."""
     torch = cuda
     before = _direct_count(mpi)
     for op, t in (("MPI_SUM", "MPI_FLOAT"), ("MPI_MAX", "MPI_DOUBLE"), ("MPI_PROD", "MPI_INT"),
@@ -807,38 +807,41 @@ def test_direct_dispatch_path(mpi, orc, cuda):
         run_pair(mpi, orc, torch, op, t, (1 << 18) + (16 // T.elem_size(t)) * 5, 31)
     mid = _direct_count(mpi)
     assert mid - before == 5, (before, mid)
-    # the full tile kernel: ragged counts, equal misalignment, small counts, other ops
-    cases = [("MPI_SUM", "MPI_FLOAT", (1 << 18) + 1, 0, 0), ("MPI_SUM", "MPI_FLOAT", 3, 0, 0),
+    cases = [("MPI_SUM", "MPI_FLOAT", (1 << 18) + 1, 0, 0), ("MPI_SUM", "MPI_FLOAT", 3, 0, 0),     # full
              ("MPI_BXOR", "MPI_INT", 1 << 18, 0, 0), ("MPI_LAND", "MPI_UNSIGNED_CHAR", 4099, 5, 5),
              ("MPI_MAXLOC", "MPI_2INT", 1001, 8, 8), ("MPI_MINLOC", "MPI_DOUBLE_INT", 33, 0, 0),
              ("MPI_SUM", "MPI_LONG_DOUBLE", 257, 0, 0), ("MPI_LXOR", "MPI_DOUBLE", 77, 8, 8),
-             ("MPI_PROD", "MPI_C_FLOAT_COMPLEX", 65537, 8, 8), ("MPI_BOR", "MPI_SHORT", 1, 2, 2)]
+             ("MPI_PROD", "MPI_C_FLOAT_COMPLEX", 65537, 8, 8), ("MPI_BOR", "MPI_SHORT", 1, 2, 2),
+             ("MPI_SUM", "MPI_FLOAT", 65539, 4, 0), ("MPI_MAX", "MPI_DOUBLE", 40000, 8, 0),            # shift
+             ("MPI_SUM", "MPI_FLOAT", 4099, 4, 0), ("MPI_MINLOC", "MPI_SHORT_INT", 99, 4, 0),          # elements
+             ("MPI_SUM", "MPI_DOUBLE", 1000, 3, 5)]                                                    # unnatural
     for k, (op, t, n, oi, oo) in enumerate(cases):
         run_pair(mpi, orc, torch, op, t, n, 40 + k, oi, oo)
     after = _direct_count(mpi)
     assert after - mid == len(cases), (mid, after)
-    # unequal alignment mod 16 and the 32-byte classes: the HIP launch
-    run_pair(mpi, orc, torch, "MPI_SUM", "MPI_FLOAT", 4099, 60, 4, 0)
+    # the 32-byte classes: the HIP launch
     run_pair(mpi, orc, torch, "MPI_SUM", "MPI_C_LONG_DOUBLE_COMPLEX", 513, 61)
+    run_pair(mpi, orc, torch, "MPI_MAXLOC", "MPI_LONG_DOUBLE_INT", 99, 62)
     assert _direct_count(mpi) == after
 
 
 @pytest.mark.parametrize("op,t", MATRIX, ids=[f"{o}-{t}" for o, t in MATRIX])
 def test_direct_dispatch_matrix(mpi, orc, cuda, op, t):
-    """Every (op, type) the reference accepts at ragged counts and equal
-    misalignment: the classes of 16 bytes or less take the direct dispatch
-    (counted), the 32-byte ones the HIP launch; all bit-exact."""
+    """Every (op, type) the reference accepts, at ragged counts, equal and
+    unequal misalignment: the classes of 16 bytes or less take the direct
+    dispatch (counted), the 32-byte ones the HIP launch; all bit-exact."""
     esz = T.elem_size(t)
+    eq = esz if 16 % esz == 0 and esz < 16 else 0
+    shapes = [(1, 0, 0), (5, eq, eq), (4099, 0, 0), ((1 << 16) + 3, 0, 0),
+              ((1 << 16) + 3, 4 if esz % 4 == 0 else 1, 0), (77, 0, 2 if esz % 2 == 0 else 1)]
     d0 = _direct_count(mpi)
-    calls = 0
-    for n, off in ((1, 0), (5, esz if 16 % esz == 0 and esz < 16 else 0), (4099, 0), ((1 << 16) + 3, 0)):
-        run_pair(mpi, orc, cuda, op, t, n, 7 + n, off, off)
-        calls += 1
+    for n, oi, oo in shapes:
+        run_pair(mpi, orc, cuda, op, t, n, 7 + n + oi, oi, oo)
     got = _direct_count(mpi) - d0
     # LAND / LOR on the reals pass check_dtype and then fail in the kernel's
     # type switch (the reference's quirk): no kernel runs
     quirk = op in ("MPI_LAND", "MPI_LOR") and t in T.REAL
-    assert got == (calls if esz <= 16 and not quirk else 0), (op, t, got)
+    assert got == (len(shapes) if esz <= 16 and not quirk else 0), (op, t, got)
 
 
 def test_direct_dispatch_many_threads_distinct_windows(mpi, cuda):

@@ -1,8 +1,8 @@
 #!/usr/bin/env python3
 """Synchronous device-resident MPI_Reduce_local latency (median of 2000 calls,
 compiled binding) for shapes the direct AQL dispatch took from the HIP launch
-path when it gained the full tile kernel: ragged counts, equal misalignment,
-the logical / bitwise / MAXLOC ops.  Run twice to compare:
+path when it gained every kernel of plan_reduce: ragged counts, equal and
+unequal misalignment, the logical / bitwise / MAXLOC ops.  Run twice to compare:
 
     python3 tools/direct_latency.py                                      # direct
     MPIR_CVAR_REDUCE_LOCAL_DISPATCH=hip python3 tools/direct_latency.py  # HIP launch
@@ -22,16 +22,20 @@ def main():
     lib = m.load()
     f = m.fast_reduce_local()
     mode = os.environ.get("MPIR_CVAR_REDUCE_LOCAL_DISPATCH", "direct")
-    cases = [("fp32 SUM", m.MPI_FLOAT, m.MPI_SUM, 4, 4, 0), ("fp32 SUM", m.MPI_FLOAT, m.MPI_SUM, 1, 4, 0),
-             ("fp32 SUM", m.MPI_FLOAT, m.MPI_SUM, 4099, 4, 0), ("fp32 SUM +4 B", m.MPI_FLOAT, m.MPI_SUM, 4096, 4, 4),
-             ("fp32 SUM", m.MPI_FLOAT, m.MPI_SUM, (1 << 20) + 7, 4, 0),
-             ("int BXOR", m.MPI_INT, m.MPI_BXOR, 4096, 4, 0), ("int LAND", m.MPI_INT, m.MPI_LAND, 4096, 4, 0),
-             ("2INT MAXLOC", m.MPI_2INT, m.MPI_MAXLOC, 4096, 8, 0)]
+    # (name, datatype, op, count, element bytes, inbuf offset, inoutbuf offset)
+    cases = [("fp32 SUM", m.MPI_FLOAT, m.MPI_SUM, 4, 4, 0, 0), ("fp32 SUM", m.MPI_FLOAT, m.MPI_SUM, 1, 4, 0, 0),
+             ("fp32 SUM", m.MPI_FLOAT, m.MPI_SUM, 4099, 4, 0, 0),
+             ("fp32 SUM +4/+4", m.MPI_FLOAT, m.MPI_SUM, 4096, 4, 4, 4),
+             ("fp32 SUM +4/0", m.MPI_FLOAT, m.MPI_SUM, 4099, 4, 4, 0),
+             ("fp32 SUM +4/0", m.MPI_FLOAT, m.MPI_SUM, 1 << 20, 4, 4, 0),
+             ("fp32 SUM", m.MPI_FLOAT, m.MPI_SUM, (1 << 20) + 7, 4, 0, 0),
+             ("int BXOR", m.MPI_INT, m.MPI_BXOR, 4096, 4, 0, 0), ("int LAND", m.MPI_INT, m.MPI_LAND, 4096, 4, 0, 0),
+             ("2INT MAXLOC", m.MPI_2INT, m.MPI_MAXLOC, 4096, 8, 0, 0)]
     torch.cuda.init()
-    for name, dt, op, n, esz, off in cases:
+    for name, dt, op, n, esz, oi, oo in cases:
         a = torch.zeros(n * esz + 64, dtype=torch.uint8, device="cuda")
         b = torch.zeros(n * esz + 64, dtype=torch.uint8, device="cuda")
-        pa, pb = a.data_ptr() + off, b.data_ptr() + off
+        pa, pb = a.data_ptr() + oo, b.data_ptr() + oi
         torch.cuda.synchronize()
         for _ in range(200):
             assert f(pb, pa, n, dt, op) == 0

@@ -26,7 +26,7 @@ hipError_t launch_elems(const void *in, void *io, uint64_t count, hipStream_t s)
     uint64_t grid = (count + kThreads - 1) / kThreads;
     if (grid > 4096) grid = 4096;
     hipLaunchKernelGGL((k_reduce_elems<Op, T, true>), dim3((unsigned)grid), dim3(kThreads), 0, s,
-                       (const char *)in, (char *)io, count);
+                       (const char *)in, (char *)io, count, grid * kThreads);
     return hipGetLastError();
 }
 
