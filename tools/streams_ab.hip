@@ -66,8 +66,26 @@ __global__ __launch_bounds__(TH) void k_ro(Args a) {
     if (x == 0x9e3779b9u) a.sink[blockIdx.x & 1023] = x;   // practically never: keeps the loads
 }
 
+// K consecutive tiles per workgroup: all K x P loads first, then the K tile
+// stores back to back (fewer, larger write bursts per workgroup); `policy`
+// is the store's cache-policy bits (2 = nt, 16 = sc1)
+template <int P, int K, int POL>
+__global__ __launch_bounds__(TH) void k_rwk(Args a) {
+    const uint64_t base0 = (uint64_t)blockIdx.x * TILE * K;
+    if (base0 >= a.vbytes) return;
+    const int off = (int)threadIdx.x * 16;
+    u32x4 v[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) v[k] = fold<P, 0>(a, base0 + (uint64_t)k * TILE, off);
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc((void *)(a.out + base0 + (uint64_t)k * TILE), 0, TILE, 0x00020000);
+        __builtin_amdgcn_raw_buffer_store_b128(v[k], ro, off, 0, POL);
+    }
+}
+
 typedef void (*kfn)(Args);
-struct Var { std::string name; kfn k; int P; int IL; };
+struct Var { std::string name; kfn k; int P; int IL; int K = 1; };
 
 int main(int argc, char **argv) {
     const size_t mib = argc > 1 ? strtoull(argv[1], 0, 10) : 32;
@@ -100,6 +118,11 @@ int main(int argc, char **argv) {
         {"rw P8", k_rw<8, 0>, 8, 0}, {"rw P8 interleaved", k_rw<8, 1>, 8, 1}, {"rw P4 interleaved", k_rw<4, 1>, 4, 1},
         {"ro P2", k_ro<2, 0>, 2, 0}, {"ro P4", k_ro<4, 0>, 4, 0}, {"ro P8", k_ro<8, 0>, 8, 0},
         {"ro P8 interleaved", k_ro<8, 1>, 8, 1},
+        {"rwk P8 K2", k_rwk<8, 2, 2>, 8, 0, 2}, {"rwk P8 K4", k_rwk<8, 4, 2>, 8, 0, 4},
+        {"rwk P8 K1 sc1", k_rwk<8, 1, 16>, 8, 0, 1}, {"rwk P8 K2 sc1", k_rwk<8, 2, 16>, 8, 0, 2},
+        {"rwk P2 K2", k_rwk<2, 2, 2>, 2, 0, 2},
+        {"rwk P1 sc1", k_rwk<1, 1, 16>, 1, 0, 1}, {"rwk P2 sc1", k_rwk<2, 1, 16>, 2, 0, 1},
+        {"rwk P4 sc1", k_rwk<4, 1, 16>, 4, 0, 1},
     };
     hipStream_t st;
     CK(hipStreamCreate(&st));
@@ -115,11 +138,37 @@ int main(int argc, char **argv) {
         }
         for (int vi : order) {
             const int s = slot++ % NS;
-            hipLaunchKernelGGL(vs[vi].k, dim3(grid), dim3(TH), 0, st, vs[vi].IL ? il[s] : sep[s]);
+            hipLaunchKernelGGL(vs[vi].k, dim3((grid + vs[vi].K - 1) / vs[vi].K), dim3(TH), 0, st, vs[vi].IL ? il[s] : sep[s]);
             CK(hipGetLastError());
             CK(hipStreamSynchronize(st));
         }
     }
     printf("%zu MiB per operand, skew %zu B, %d sets, %d rounds\n", mib, skew, NS, rounds);
+    // BATCH=1: each variant timed over `rounds` back-to-back launches (sets
+    // rotating) between two events, so stores an sc1 policy leaves dirty in the
+    // Infinity Cache are paid by the batch, not by whichever kernel runs next
+    if (getenv("BATCH")) {
+        hipEvent_t e0, e1;
+        CK(hipEventCreate(&e0));
+        CK(hipEventCreate(&e1));
+        for (int pass = 0; pass < 2; ++pass) {
+            for (size_t vi = 0; vi < vs.size(); ++vi) {
+                const Var &v = vs[vi];
+                const unsigned g = (grid + v.K - 1) / v.K;
+                for (int w = 0; w < 3; ++w) hipLaunchKernelGGL(v.k, dim3(g), dim3(TH), 0, st, v.IL ? il[w % NS] : sep[w % NS]);
+                CK(hipEventRecord(e0, st));
+                for (int r = 0; r < rounds; ++r)
+                    hipLaunchKernelGGL(v.k, dim3(g), dim3(TH), 0, st, v.IL ? il[r % NS] : sep[r % NS]);
+                CK(hipEventRecord(e1, st));
+                CK(hipStreamSynchronize(st));
+                float ms = 0;
+                CK(hipEventElapsedTime(&ms, e0, e1));
+                const double us = ms * 1e3 / rounds;
+                const bool ro = v.name.rfind("ro", 0) == 0;
+                const double alg = (double)(v.P + (ro ? 0 : 1)) * bytes;
+                if (pass) printf("batch %-20s %8.2f us per launch  frac %.3f\n", v.name.c_str(), us, alg / us / 8e6);
+            }
+        }
+    }
     return 0;
 }

@@ -23,13 +23,15 @@ for r in csv.DictReader(open(path)):
     d.setdefault(r["Kernel_Name"], []).append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
 rows = []
 for name, v in d.items():
-    m = re.search(r"k_(rw|ro)<(\d+), (\d+)>", name)
+    m = re.search(r"k_(rwk|rw|ro)<(\d+), (\d+)(?:, (\d+))?>", name)
     if not m:
         continue
     kind, p, il = m.group(1), int(m.group(2)), int(m.group(3))
+    if kind == "rwk":
+        kind, il = "rw K%d pol%s" % (il, m.group(4)), 0
     v = v[2:] or v
     med = statistics.median(v)
-    alg = (p + (1 if kind == "rw" else 0)) * mib * 1048576
+    alg = (p + (1 if kind.startswith("rw") else 0)) * mib * 1048576
     rows.append((kind, p, il, med, alg / med / 8e6))
 for kind, p, il, med, f in sorted(rows):
     print(f"  {kind} P{p} {'interleaved' if il else 'strided    '}  median {med:8.2f} us  frac {f:.3f}")
