@@ -163,6 +163,10 @@ int main(int argc, char **argv) {
         {"TREE8 f32 U1 T1024 gap8", 4, &launch_mx<float, true, 1, 1024, 8>},
         {"TREE8 f32 U2 T512 gap4", 4, &launch_mx<float, true, 2, 512, 4>},
         {"TREE8 f32 U2 T256 gap4", 4, &launch_mx<float, true, 2, 256, 4>},
+        {"TREE8 f32 U4 T256 gap4", 4, &launch_mx<float, true, 4, 256, 4>},
+        {"TREE8 f32 U4 T256 gap8", 4, &launch_mx<float, true, 4, 256, 8>},
+        {"TREE8 f32 U4 T128 gap4", 4, &launch_mx<float, true, 4, 128, 4>},
+        {"TREE8 f32 U2 T1024 gap4", 4, &launch_mx<float, true, 2, 1024, 4>},
     };
     else vs = {
         {"CHAIN8 f16 product (U1 T1024)", 2, &launch_combine_p<OpSum, _Float16, 8, false>},
@@ -213,6 +217,30 @@ int main(int argc, char **argv) {
         const float med = dur[i][dur[i].size() / 2];
         printf("  %-34s median %7.2f us  p10 %7.2f  frac %.4f\n", vs[i].name.c_str(), med, dur[i][dur[i].size() / 10],
                9.0 * bytes / (med * 1e-6) / 8e12);
+    }
+    // BATCH=1: each variant over `rounds` back-to-back launches between two
+    // events (sets rotating): the steady state, with any write-back an sc1
+    // store policy defers paid inside the batch
+    if (getenv("BATCH")) {
+        for (int pass = 0; pass < 2; ++pass)
+            for (size_t vi = 0; vi < vs.size(); ++vi) {
+                auto launch = [&](int k) {
+                    const int s = k % NS;
+                    const void *ptr[P];
+                    for (int j = 0; j < P; ++j) ptr[j] = ins[s * P + j];
+                    CK(vs[vi].fn(ptr, outs[s], bytes / vs[vi].esz, st));
+                };
+                for (int w = 0; w < 3; ++w) launch(w);
+                CK(hipEventRecord(e0, st));
+                for (int r = 0; r < rounds; ++r) launch(r);
+                CK(hipEventRecord(e1, st));
+                CK(hipStreamSynchronize(st));
+                float ms = 0;
+                CK(hipEventElapsedTime(&ms, e0, e1));
+                const double us = ms * 1e3 / rounds;
+                if (pass) printf("  batch %-34s %7.2f us per launch  frac %.4f\n", vs[vi].name.c_str(), us,
+                                 9.0 * bytes / (us * 1e-6) / 8e12);
+            }
     }
     return 0;
 }
