@@ -306,13 +306,19 @@ void init_dev(int dev, DevState &d) {
                 const std::string sym = std::string(kPlanPrefix[kind]) + op_name(op) + "_" + elem_name(e) + ".kd";
                 hsa_executable_symbol_t s;
                 uint64_t ko = 0;
-                uint32_t kas = 0;
+                uint32_t kas = 0, lds = 1, priv = 1;
                 if (hsa_executable_get_symbol_by_name(exe, sym.c_str(), &f.gpu, &s) != HSA_STATUS_SUCCESS) continue;
+                // the packets carry no LDS or scratch: a kernel that needs either
+                // (or reads arguments the host does not write) stays on the HIP path
                 if (hsa_executable_symbol_get_info(s, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_OBJECT, &ko) !=
                         HSA_STATUS_SUCCESS ||
                     hsa_executable_symbol_get_info(s, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_KERNARG_SEGMENT_SIZE, &kas) !=
                         HSA_STATUS_SUCCESS ||
-                    kas != kPlanArgBytes[kind])
+                    hsa_executable_symbol_get_info(s, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_GROUP_SEGMENT_SIZE, &lds) !=
+                        HSA_STATUS_SUCCESS ||
+                    hsa_executable_symbol_get_info(s, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_PRIVATE_SEGMENT_SIZE, &priv) !=
+                        HSA_STATUS_SUCCESS ||
+                    kas != kPlanArgBytes[kind] || lds != 0 || priv != 0)
                     continue;
                 d.kobj[kind][op][e] = ko;
                 ++found;
