@@ -62,7 +62,7 @@ def test_roofline_is_self_consistent(line):
 
 def test_live_kernel_time_agrees_with_rocprof(line):
     """bench.py times the kernel the synchronous call runs; rocprofv3's
-    --kernel-trace --stats average for that kernel (profiles/r02c_kernel_stats.csv,
+    --kernel-trace --stats average for that kernel (profiles/r02d_kernel_stats.csv,
     summarised in pmc_traffic.json) must agree with it."""
     r = line["roofline"]
     with open(os.path.join(ROOT, "profiles", "pmc_traffic.json")) as f:
