@@ -423,12 +423,22 @@ def main():
     if world != args.gpus:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world} (launched by an external launcher); "
               f"measuring WORLD_SIZE ranks", file=sys.stderr)
-    torch.cuda.set_device(local)
+    # BENCH_TEST_SHARE_GPU=1 (test only): N ranks on the GPUs there are
+    # (rank -> device local % count) with a gloo process group, since RCCL
+    # refuses two ranks on one GPU -- rehearses the whole N > 1 path (launch,
+    # per-rank direct dispatch, extras, the collectives child's error report)
+    # on a one-GPU box.  Never a measurement of N GPUs.
+    share = os.environ.get("BENCH_TEST_SHARE_GPU") == "1"
+    dev = local % torch.cuda.device_count() if share else local
+    torch.cuda.set_device(dev)
     # BENCH_TEST_PG=1 (test only): the N > 1 plumbing -- RCCL process group,
     # barriers, max over ranks -- at WORLD_SIZE 1, to rehearse it on one GPU
     use_pg = world > 1 or os.environ.get("BENCH_TEST_PG") == "1"
     if use_pg:
-        dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
+        if share:
+            dist.init_process_group(backend="gloo")
+        else:
+            dist.init_process_group(backend="nccl", device_id=torch.device("cuda", dev))
 
     def barrier():
         if use_pg:
@@ -437,7 +447,7 @@ def main():
     def max_over_ranks(x: float) -> float:
         if not use_pg:
             return x
-        t = torch.tensor([x], dtype=torch.float64, device="cuda")
+        t = torch.tensor([x], dtype=torch.float64, device="cpu" if share else "cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
 
@@ -502,6 +512,10 @@ def main():
                     # the buffer rate count * sizeof(T) / t, for readability
                     "buffer_GiBps": round(value / world / 3, 1)},
     }
+
+    if share:
+        out["data"] = "REHEARSAL (BENCH_TEST_SHARE_GPU): %d ranks on %d GPU(s), not a measurement" % (
+            world, torch.cuda.device_count())
 
     if not args.no_extras:
         # ---- roofline: the synchronous call's kernel, timed by the CP's dispatch
@@ -613,7 +627,7 @@ def main():
         del ha, hb, pa, pb
 
     if args.collectives == "on" or (args.collectives == "auto" and world > 1 and not args.no_extras):
-        coll = run_collectives_child(rank, world, local, barrier)
+        coll = run_collectives_child(rank, world, dev, barrier)
         if rank == 0:
             out["collectives"] = coll
 
