@@ -282,9 +282,19 @@ def config2(m, lib, pairs, stream, k: int, w: int):
         assert lib.MPIX_Reduce_local_stream(b.data_ptr(), a.data_ptr(), count, m.MPI_FLOAT, m.MPI_SUM,
                                             stream.cuda_stream) == 0
 
+    # the synchronous call as the headline step makes it: compiled binding,
+    # arguments built once (ctypes + per-call tensor slicing cost ~2.5 us of
+    # Python per call, 7 % of a 64 MiB call)
+    try:
+        reduce_local = m.fast_reduce_local()
+    except ImportError:
+        reduce_local = lib.MPI_Reduce_local
+    call_args = [(b.data_ptr(), a.data_ptr(), count, m.MPI_FLOAT, m.MPI_SUM) for a, b in wins]
+
     def call(i):
-        a, b = wins[i % len(wins)]
-        assert lib.MPI_Reduce_local(b.data_ptr(), a.data_ptr(), count, m.MPI_FLOAT, m.MPI_SUM) == 0
+        rc = reduce_local(*call_args[i % len(call_args)])
+        if rc:
+            raise RuntimeError(m.error_string(rc))
     alg = 3 * count * 4
     out = {"windows": len(wins)}
     ns = direct_kernel_ns(lib, call, k, w)

@@ -184,9 +184,11 @@ int main(int argc, char **argv) {
     memset(dec, 0, 4096);
     hdp_flush(true);
     // kernarg slots in VRAM: 64 windows for plain (cached), 64 ring slots for gates
-    char *karg = (char *)vram_alloc(128 * 128);
+    char *karg = (char *)vram_alloc(192 * 128);
     std::vector<hsa_signal_t> sig(64);
     for (auto &s : sig) HK(hsa_signal_create(1, 0, nullptr, &s));
+    std::vector<hsa_signal_t> sigb(64);
+    for (auto &s : sigb) HK(hsa_signal_create(1, 0, nullptr, &s));
     float *hostbuf = (float *)fine_alloc(4096);
 
     const uint64_t lead = 10000, follow = 1000000;   // 100 us, 10 ms at 100 MHz
@@ -201,11 +203,20 @@ int main(int argc, char **argv) {
             PlainArgs a{in[p] + off, io[p] + off, vbytes, 0};
             memcpy(karg + w * 128, &a, sizeof a);
         }
+        // split mode: the pre-posted gate covers the first wave of tiles (kFirst
+        // workgroups, one per resident slot), a plain kernel posted at call time the rest
+        const uint32_t kFirst = 2048;
+        const uint64_t first_bytes = std::min<uint64_t>(vbytes, (uint64_t)kFirst * 16384);
+        for (int w = 0; w < nwin && w < 64; ++w) {
+            const int p = w % NP, off = (w / NP) * (int)(vbytes / 4);
+            PlainArgs a{(char *)(in[p] + off) + first_bytes, (char *)(io[p] + off) + first_bytes, vbytes - first_bytes, 0};
+            memcpy(karg + (128 + w) * 128, &a, sizeof a);
+        }
         hdp_flush(true);
         struct Mode { int kind; uint32_t sleep; };
         std::vector<Mode> modes{{0, 0}};
-        for (uint32_t sl : sleeps) { modes.push_back({1, sl}); modes.push_back({2, sl}); }
-        static const char *kname[3] = {"plain", "gate", "direct"};
+        for (uint32_t sl : sleeps) { modes.push_back({1, sl}); modes.push_back({2, sl}); modes.push_back({3, sl}); }
+        static const char *kname[4] = {"plain", "gate", "direct", "split"};
         for (int round = 0; round < 2; ++round) {
             for (const Mode &md : modes) {
                 const int mode = md.kind;
@@ -226,7 +237,7 @@ int main(int argc, char **argv) {
                         DirectArgs g{seqs, mail, kk, 0, lead, md.sleep, 0};
                         memcpy(slot, &g, sizeof g);
                         hdp_flush(true);
-                        post(ko_direct, slot, grid, sig[kk & 63]);
+                        post(ko_direct, slot, mode == 3 ? std::min(grid, kFirst) : grid, sig[kk & 63]);
                     }
                 };
                 if (mode != 0) arm(++gate_k);
@@ -242,17 +253,20 @@ int main(int argc, char **argv) {
                         const int p = w % NP, off = (w / NP) * (int)(vbytes / 4);
                         mail->in = (uint64_t)(in[p] + off);
                         mail->io = (uint64_t)(io[p] + off);
-                        mail->vbytes = vbytes;
+                        mail->vbytes = mode == 3 ? first_bytes : vbytes;
                         mail->keep = 0;
                         _mm_sfence();
                         if (mode == 1) {
                             __atomic_store_n(&mail->seq, k, __ATOMIC_RELEASE);
                         } else {
-                            for (int r = 0; r < 8; ++r) __atomic_store_n(seqs + r * 32, k, __ATOMIC_RELEASE);
+                            for (int r = 0; r < 8; ++r) __atomic_store_n(seqs + r * 32, k, __ATOMIC_RELEASE);   // direct, split
                         }
                         hdp_flush(false);
+                        const bool rest = mode == 3 && vbytes > first_bytes;
+                        if (rest) post(ko_plain, karg + (128 + w) * 128, grid - kFirst, sigb[c & 63]);
                         arm(++gate_k);          // the next call's gate, queued behind this one
                         if (!wait_sig(sig[k & 63])) { lost++; break; }
+                        if (rest && !wait_sig(sigb[c & 63])) { lost++; break; }
                         if (mode == 1) {
                             const uint32_t v = __atomic_load_n(outcome + (k & 63) * 32, __ATOMIC_ACQUIRE);
                             if (v != ((k << 1) | 1u)) fails++;
