@@ -9,6 +9,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sched.h>
 #include <unistd.h>
 
 #include <algorithm>
@@ -226,12 +227,12 @@ int get_bounce(int dev, size_t bytes, char **out) {
 // worker threads: one thread moves 31-33 GB/s between pageable and pinned
 // memory on the MI355X host, four 83-86 GB/s (tools/memcpy_bw.cpp,
 // profiles/r01s3_memcpy_bw.log) -- more than the ~51 GB/s a PCIe Gen5 x16
-// upload takes.  MPIR_CVAR_REDUCE_LOCAL_STAGE_THREADS (default 4; 1 = the
-// calling thread alone).  The pool is never torn down: its idle workers end
+// upload takes; the host combine uses every thread (copy_pool() below).
+// MPIR_CVAR_REDUCE_LOCAL_STAGE_THREADS (1 = the calling thread alone).  The pool is never torn down: its idle workers end
 // with the process, so exit never waits on them.
 class CopyPool {
   public:
-    explicit CopyPool(int nthreads) : n_(nthreads), pid_(getpid()) {
+    CopyPool(int nthreads, int copy_parts) : n_(nthreads), copy_n_(std::min(nthreads, copy_parts)), pid_(getpid()) {
         for (int i = 1; i < n_; ++i) std::thread([this] { work(); }).detach();
     }
     int threads() const { return n_; }
@@ -256,13 +257,18 @@ class CopyPool {
             pending_ = nparts - 1;
             ++gen_;
         }
-        cv_.notify_all();
+        // wake only as many workers as there are parts for (a copy of 4
+        // parts on a 16-thread pool: +9 us at 1 MiB with notify_all)
+        for (size_t k = 1; k < nparts && k < (size_t)n_; ++k) cv_.notify_one();
         fn(ctx, 0);
         std::unique_lock<std::mutex> lk(mu_);
         done_.wait(lk, [this] { return pending_ == 0; });
     }
+    // copies split into at most copy_n_ parts: PCIe, not the host's memory,
+    // bounds them, and more parts only add wake-ups (host->device 1 MiB 52 ->
+    // 74 us with 16 parts, profiles/r02/host_threads_ab.log)
     void copy(char *dst, const char *src, size_t bytes, size_t min_split = (size_t)1 << 20) {
-        if (n_ <= 1 || bytes < min_split || getpid() != pid_) {
+        if (copy_n_ <= 1 || bytes < min_split || getpid() != pid_) {
             memcpy(dst, src, bytes);
             return;
         }
@@ -270,7 +276,7 @@ class CopyPool {
             char *d;
             const char *s;
             size_t bytes, part;
-        } c{dst, src, bytes, ((bytes + n_ - 1) / n_ + 63) & ~(size_t)63};
+        } c{dst, src, bytes, ((bytes + copy_n_ - 1) / copy_n_ + 63) & ~(size_t)63};
         run((bytes + c.part - 1) / c.part, [](void *p, size_t k) {
             const C *c = static_cast<const C *>(p);
             const size_t o = k * c->part;
@@ -294,7 +300,7 @@ class CopyPool {
             }
         }
     }
-    int n_;
+    int n_, copy_n_;
     pid_t pid_;
     std::mutex job_mu_, mu_;
     std::condition_variable cv_, done_;
@@ -304,11 +310,35 @@ class CopyPool {
     uint64_t gen_ = 0;
 };
 
+// CPUs this process may run on: its affinity mask, capped by a cgroup v2 CPU
+// quota (cpu.max "quota period"), as a container or batch job sets it.
+int usable_cpus() {
+    cpu_set_t set;
+    int n = sched_getaffinity(0, sizeof set, &set) == 0 ? CPU_COUNT(&set) : 1;
+    if (FILE *f = fopen("/sys/fs/cgroup/cpu.max", "r")) {
+        char quota[32];
+        long period = 0;
+        if (fscanf(f, "%31s %ld", quota, &period) == 2 && strcmp(quota, "max") != 0 && period > 0) {
+            const long q = (atol(quota) + period - 1) / period;
+            if (q >= 1 && q < n) n = (int)q;
+        }
+        fclose(f);
+    }
+    return n;
+}
+
+// Default pool size: the usable CPUs, 4 to 16, for the host combine of large
+// both-host operands, which is memory-bound and scales with threads (256 MiB
+// fp32 SUM on the MI355X host, 16-CPU quota: 131-136 GiB/s on 4 threads,
+// 259-299 on 16; profiles/r02/host_threads_ab.log).  Copies (bounce path,
+// mixed-residency slots) keep to 4 parts, which already outrun a PCIe upload.
+// MPIR_CVAR_REDUCE_LOCAL_STAGE_THREADS sets both.
 CopyPool &copy_pool() {
     static CopyPool *pool = [] {
         const char *e = getenv("MPIR_CVAR_REDUCE_LOCAL_STAGE_THREADS");
-        const int n = e ? atoi(e) : 4;
-        return new CopyPool(n >= 1 && n <= 64 ? n : 4);
+        int n = e ? atoi(e) : std::min(16, std::max(4, usable_cpus()));
+        if (n < 1 || n > 64) n = 4;
+        return new CopyPool(n, e ? n : 4);
     }();
     return *pool;
 }
@@ -657,7 +687,9 @@ int MPIR_Hip_reduce(const void *inbuf, void *inoutbuf, uint64_t count, int op, i
             char *io;
             uint64_t n, part, unit;
         } h{g_table[op][elem].host, static_cast<const char *>(inbuf), static_cast<char *>(inoutbuf), n, 0, unit};
-        const uint64_t per = (n + copy_pool().threads() - 1) / copy_pool().threads();
+        // parts of at least 256 KiB: a worker's wake-up costs a few us
+        const uint64_t per = std::max<uint64_t>((n + copy_pool().threads() - 1) / copy_pool().threads(),
+                                                ((uint64_t)256 << 10) / unit);
         const uint64_t grain = unit >= 64 ? 1 : 64 / unit;
         h.part = (per + grain - 1) / grain * grain;
         copy_pool().run((size_t)((n + h.part - 1) / h.part), [](void *p, size_t k) {
