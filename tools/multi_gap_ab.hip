@@ -113,6 +113,63 @@ hipError_t launch_rev(const void *const *ins, void *out, uint64_t count, hipStre
     return hipGetLastError();
 }
 
+
+// software-pipelined: each workgroup folds NT consecutive tiles (U = 1), the
+// eight loads of tile t+1 issued before tile t's combine and store, so stores
+// leave the workgroup between loads instead of in one burst at its end
+template <class T, bool TREE, int TH, int NT>
+__global__ __launch_bounds__(TH) void k_pipe(MultiArgs a) {
+    constexpr int P = 8;
+    constexpr uint32_t tile = TH * 16;
+    const int t = (int)threadIdx.x;
+    const int off = (t >> 6) * 1024 + (t & 63) * 16;
+    const uint64_t base0 = (uint64_t)blockIdx.x * tile * NT;
+    u32x4 x[2][P];
+    auto load = [&](int buf, uint64_t base) {
+        const uint64_t left = base < a.vbytes ? a.vbytes - base : 0;
+        const int nrec = (int)(left < tile ? left : tile);
+#pragma unroll
+        for (int j = 0; j < P; ++j) {
+            __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void *)(a.in[j] + base), 0, nrec, 0x00020000);
+            x[buf][j] = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, kCachePolicyNT);
+            if ((j + 1) % 4 == 0 && j + 1 < P) issue_gap();
+        }
+    };
+    if (base0 >= a.vbytes) return;
+    load(0, base0);
+#pragma unroll
+    for (int k = 0; k < NT; ++k) {
+        const uint64_t base = base0 + (uint64_t)k * tile;
+        if (k + 1 < NT) load((k + 1) & 1, base + tile);
+        if (base >= a.vbytes) break;
+        const uint64_t left = a.vbytes - base;
+        const int nrec = (int)(left < tile ? left : tile);
+        Pack16<T> pk[P];
+#pragma unroll
+        for (int j = 0; j < P; ++j) pk[j] = __builtin_bit_cast(Pack16<T>, x[k & 1][j]);
+        Pack16<T> res;
+#pragma unroll
+        for (int e = 0; e < (int)(16 / sizeof(T)); ++e) {
+            T v[P];
+#pragma unroll
+            for (int j = 0; j < P; ++j) v[j] = pk[j].e[e];
+            res.e[e] = fold_fast<OpSum, T, P, TREE>(v);
+        }
+        __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc((void *)(a.out + base), 0, nrec, 0x00020000);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, res), ro, off, 0, kCachePolicyNT);
+    }
+}
+template <class T, bool TREE, int TH, int NT>
+hipError_t launch_pipe(const void *const *ins, void *out, uint64_t count, hipStream_t s) {
+    MultiArgs a{};
+    for (int j = 0; j < 8; ++j) a.in[j] = static_cast<const char *>(ins[j]);
+    a.out = static_cast<char *>(out);
+    a.vbytes = count * sizeof(T);
+    constexpr uint64_t span = (uint64_t)TH * 16 * NT;
+    hipLaunchKernelGGL((k_pipe<T, TREE, TH, NT>), dim3((unsigned)((a.vbytes + span - 1) / span)), dim3(TH), 0, s, a);
+    return hipGetLastError();
+}
+
 typedef hipError_t (*mfn)(const void *const *, void *, uint64_t, hipStream_t);
 
 template <class T, bool TREE, int U, int TH, int GAP, int P = 8>
@@ -167,6 +224,11 @@ int main(int argc, char **argv) {
         {"TREE8 f32 U4 T256 gap8", 4, &launch_mx<float, true, 4, 256, 8>},
         {"TREE8 f32 U4 T128 gap4", 4, &launch_mx<float, true, 4, 128, 4>},
         {"TREE8 f32 U2 T1024 gap4", 4, &launch_mx<float, true, 2, 1024, 4>},
+        {"TREE8 f32 pipe2 T256", 4, &launch_pipe<float, true, 256, 2>},
+        {"TREE8 f32 pipe4 T256", 4, &launch_pipe<float, true, 256, 4>},
+        {"TREE8 f32 pipe2 T512", 4, &launch_pipe<float, true, 512, 2>},
+        {"TREE8 f32 pipe4 T512", 4, &launch_pipe<float, true, 512, 4>},
+        {"TREE8 f32 pipe8 T256", 4, &launch_pipe<float, true, 256, 8>},
     };
     else vs = {
         {"CHAIN8 f16 product (U1 T1024)", 2, &launch_combine_p<OpSum, _Float16, 8, false>},
@@ -181,6 +243,9 @@ int main(int argc, char **argv) {
         {"CHAIN8 f16 U1 T1024 gap0", 2, &launch_mx<_Float16, false, 1, 1024, 0>},
         {"CHAIN8 f16 U1 T1024 gap8", 2, &launch_mx<_Float16, false, 1, 1024, 8>},
         {"CHAIN8 f16 U2 T512 gap4", 2, &launch_mx<_Float16, false, 2, 512, 4>},
+        {"CHAIN8 f16 pipe2 T256", 2, &launch_pipe<_Float16, false, 256, 2>},
+        {"CHAIN8 f16 pipe4 T256", 2, &launch_pipe<_Float16, false, 256, 4>},
+        {"CHAIN8 f16 pipe4 T512", 2, &launch_pipe<_Float16, false, 512, 4>},
     };
     std::vector<std::vector<float>> dur(vs.size());
     hipEvent_t e0, e1;
