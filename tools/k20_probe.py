@@ -23,6 +23,7 @@ ap.add_argument("--reps", type=int, default=6)
 ap.add_argument("--warmup", type=int, default=5)
 ap.add_argument("--steps", type=int, default=20)
 ap.add_argument("--pre-ms", type=float, default=0.0, help="GPU work (pair fills) before the first warm-up call")
+ap.add_argument("--mib", type=int, default=256, help="MiB per operand; below 256 the pairs are cut into windows")
 args = ap.parse_args()
 
 import torch
@@ -42,8 +43,11 @@ if args.pre_ms > 0:
         for a, b in pairs:
             a.mul_(1.0)
     torch.cuda.synchronize()
-call_args = [(b.data_ptr(), a.data_ptr(), count, m.MPI_FLOAT, m.MPI_SUM) for a, b in pairs]
-alg = 3 * count * 4
+wcount = args.mib << 18
+nwin = count // wcount
+call_args = [(b.data_ptr() + j * wcount * 4, a.data_ptr() + j * wcount * 4, wcount, m.MPI_FLOAT, m.MPI_SUM)
+             for a, b in pairs for j in range(nwin)]
+alg = 3 * wcount * 4
 
 # idle synchronize cost
 ts = []
@@ -57,14 +61,14 @@ print(f"idle torch.cuda.synchronize: median {ts[25]:.2f} us, max {ts[-1]:.2f} us
 for rep in range(args.reps):
     lib.MPIR_Hip_direct_profile(1)
     for i in range(args.warmup):
-        fast(*call_args[i % 4])
+        fast(*call_args[i % len(call_args)])
     torch.cuda.synchronize()
     torch.cuda.synchronize()
     wall, kern = [], []
     t0 = time.perf_counter()
     for i in range(args.steps):
         c0 = time.perf_counter()
-        fast(*call_args[(args.warmup + i) % 4])
+        fast(*call_args[(args.warmup + i) % len(call_args)])
         wall.append((time.perf_counter() - c0) * 1e6)
         kern.append(lib.MPIR_Hip_direct_last_kernel_ns() * 1e-3)
     s0 = time.perf_counter()
