@@ -33,7 +33,7 @@
 // system-scope acquire costs ~7 us of body, aql_sig_nt_sys) and a
 // system-scope release, so the result is visible to every agent -- SDMA
 // copies and the host included -- when the signal fires.  One queue per
-// device, shared by the threads; a mutex orders packet publication (single
+// device (plus its timestamped twin for profiled calls), shared by the threads; a mutex orders packet publication (single
 // producer at a time, doorbell monotonic); no barrier bit, so concurrent
 // threads' kernels overlap; each thread waits on its own signal.
 // MPIR_CVAR_REDUCE_LOCAL_DISPATCH=hip turns the path off.
@@ -90,7 +90,8 @@ struct DevState {
     bool ok = false;
     int state = 0;          // 0 not tried, 1 ready, < 0 the init step that failed (MPIR_Hip_direct_state)
     hsa_agent_t agent{};
-    hsa_queue_t *queue = nullptr;
+    hsa_queue_t *queue = nullptr;               // the calls' queue (no dispatch timestamps)
+    hsa_queue_t *pqueue = nullptr;              // the same, timestamps on: calls while profiling is on
     char *karg = nullptr;                       // kKargSlots x kKargSlotBytes, VRAM, host-written
     uint32_t kslot = 0;                         // next ring slot to try (under `publish`)
     std::atomic<int> ring_busy[kRingSlots] = {};  // a ring slot's dispatch is in flight
@@ -128,12 +129,19 @@ int mode() {
     return m;
 }
 
-// MPIR_CVAR_REDUCE_LOCAL_DIRECT_TIMESTAMPS (default 1): the direct queue
-// records dispatch start / end timestamps from its creation
+// Dispatch timestamps cost the synchronous call ~0.4 us at 256 MiB and ~0.9 us
+// at 64 MiB (the CP writes start / end times per packet; alternated processes,
+// tools/ts_ab.sh, profiles/r02/ts_ab.log), and switching them on for a live
+// queue does not take effect (tools/ts_enable_probe.py).  So the calls' queue
+// runs without them and a second queue, created with them on, takes the calls
+// made while MPIR_Hip_direct_profile is on (the bench's roofline readout: the
+// same kernel object, plan and arguments).
+// MPIR_CVAR_REDUCE_LOCAL_DIRECT_TIMESTAMPS=1 turns them on for the calls' queue
+// too (the round-2 behaviour, for A/Bs).
 int timestamps() {
     static const int t = [] {
         const char *e = getenv("MPIR_CVAR_REDUCE_LOCAL_DIRECT_TIMESTAMPS");
-        return e ? (atoi(e) != 0) : 1;
+        return e ? (atoi(e) != 0) : 0;
     }();
     return t;
 }
@@ -340,10 +348,15 @@ void init_dev(int dev, DevState &d) {
         hsa_amd_memory_pool_free(kp);
         return;
     }
+    if (hsa_queue_create(f.gpu, kQueueSize, HSA_QUEUE_TYPE_MULTI, queue_error_cb, &d, UINT32_MAX, UINT32_MAX,
+                         &d.pqueue) != HSA_STATUS_SUCCESS) {
+        hsa_queue_destroy(d.queue);
+        hsa_amd_memory_pool_free(kp);
+        return;
+    }
     d.agent = f.gpu;
-    // dispatch timestamps on from the start: enabling them on a live queue
-    // takes effect only some time later (tools/direct_probe.py); they are read
-    // only while MPIR_Hip_direct_profile is on
+    // timestamps on from creation (see timestamps())
+    hsa_amd_profiling_set_profiler_enabled(d.pqueue, 1);
     if (timestamps()) hsa_amd_profiling_set_profiler_enabled(d.queue, 1);
     if (!g_ts_freq) hsa_system_get_info(HSA_SYSTEM_INFO_TIMESTAMP_FREQUENCY, &g_ts_freq);
     d.karg = static_cast<char *>(kp);
@@ -477,7 +490,7 @@ int direct_reduce(int dev, int op, int elem, const ReducePlan &p, int *rc) {
             *d.hdp = 1u;        // HDP flush: the BAR writes land in VRAM before the CP reads them
             (void)*d.hdp;
         }
-        hsa_queue_t *q = d.queue;
+        hsa_queue_t *q = prof ? d.pqueue : d.queue;
         const uint64_t idx = hsa_queue_load_write_index_relaxed(q);
         while (idx - hsa_queue_load_read_index_scacquire(q) >= q->size) _mm_pause();
         hsa_kernel_dispatch_packet_t *p = (hsa_kernel_dispatch_packet_t *)q->base_address + (idx & (q->size - 1));
@@ -531,12 +544,7 @@ int direct_reduce(int dev, int op, int elem, const ReducePlan &p, int *rc) {
 
 uint64_t direct_calls() { return g_direct_calls.load(std::memory_order_relaxed); }
 
-void direct_profile(int on) {
-    g_profile.store(on ? 1 : 0);
-    if (!timestamps())
-        for (int i = 0; i < kMaxDirectDev; ++i)
-            if (g_dev[i].ok) hsa_amd_profiling_set_profiler_enabled(g_dev[i].queue, on ? 1 : 0);
-}
+void direct_profile(int on) { g_profile.store(on ? 1 : 0); }
 
 uint64_t direct_last_kernel_ns() { return t_last_kernel_ns; }
 
