@@ -215,9 +215,11 @@ int main(int argc, char **argv) {
         hdp_flush(true);
         struct Mode { int kind; uint32_t sleep; };
         std::vector<Mode> modes{{0, 0}};
-        for (uint32_t sl : sleeps) { modes.push_back({1, sl}); modes.push_back({2, sl}); modes.push_back({3, sl}); }
+        if (!getenv("PLAIN_ONLY"))
+            for (uint32_t sl : sleeps) { modes.push_back({1, sl}); modes.push_back({2, sl}); modes.push_back({3, sl}); }
         static const char *kname[4] = {"plain", "gate", "direct", "split"};
-        for (int round = 0; round < 2; ++round) {
+        const int nrounds = getenv("ROUNDS") ? atoi(getenv("ROUNDS")) : 2;
+        for (int round = 0; round < nrounds; ++round) {
             for (const Mode &md : modes) {
                 const int mode = md.kind;
                 for (int i = 0; i < NP; ++i) HK(hsa_amd_memory_fill(io[i], 0u, big / 4));
