@@ -444,11 +444,28 @@ def main():
     # BENCH_TEST_PG=1 (test only): the N > 1 plumbing -- RCCL process group,
     # barriers, max over ranks -- at WORLD_SIZE 1, to rehearse it on one GPU
     use_pg = world > 1 or os.environ.get("BENCH_TEST_PG") == "1"
+    pg_backend = None
     if use_pg:
         if share:
+            pg_backend = "gloo"
             dist.init_process_group(backend="gloo")
         else:
-            dist.init_process_group(backend="nccl", device_id=torch.device("cuda", dev))
+            # the group only carries the barriers and the max over ranks (no data
+            # path collective): should RCCL fail to come up, a CPU (gloo) group
+            # serves the same timing protocol rather than losing the run
+            try:
+                dist.init_process_group(backend="nccl", device_id=torch.device("cuda", dev))
+                pg_backend = "nccl"
+            except Exception as exc:       # noqa: BLE001
+                print(f"warning: RCCL process group failed ({exc}); barriers over gloo", file=sys.stderr)
+                if dist.is_initialized():
+                    dist.destroy_process_group()
+                addr = os.environ.get("MASTER_ADDR", "127.0.0.1")
+                port = int(os.environ.get("MASTER_PORT", "29500")) + 1
+                dist.init_process_group(backend="gloo", init_method=f"tcp://{addr}:{port}", rank=rank,
+                                        world_size=world)
+                pg_backend = "gloo"
+    cpu_pg = pg_backend == "gloo"
 
     def barrier():
         if use_pg:
@@ -457,7 +474,7 @@ def main():
     def max_over_ranks(x: float) -> float:
         if not use_pg:
             return x
-        t = torch.tensor([x], dtype=torch.float64, device="cpu" if share else "cuda")
+        t = torch.tensor([x], dtype=torch.float64, device="cpu" if cpu_pg else "cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
 
@@ -515,6 +532,7 @@ def main():
             "api": "MPI_Reduce_local (C ABI, synchronous; called through the " + binding + ")",
             "parallelism": "replica-per-gpu (no data-path collective)",
             "runtime": {"HSA_ALLOCATE_QUEUE_DEV_MEM": os.environ.get("HSA_ALLOCATE_QUEUE_DEV_MEM", "")},
+            "process_group": pg_backend,
         },
         # the synchronous call per GPU (launch + completion included) against the HBM peak
         "per_gpu": {"GiBps": round(value / world, 1),
