@@ -45,10 +45,15 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <pthread.h>
+#include <sched.h>
+#include <sys/prctl.h>
+#include <time.h>
 
 #include <atomic>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "mpir_hip_reduce.h"
@@ -100,6 +105,16 @@ struct DevState {
     uint64_t kobj[kPlanKinds][MPIR_HIP_NOPS][MPIR_HIP_NELEMS] = {};   // by plan kind (kPlanPrefix)
     std::mutex publish;
     std::atomic<int> queue_error{0};
+    // keep-alive (keepalive_us()): its queue and no-op kernargs; on a line of
+    // their own, the monotonic time of the last call's end or keep-alive packet
+    // and whether a call is in flight (a busy CP is not idle: no keep-alive
+    // then).  Plain stores on the call path, no read-modify-write.
+    hsa_queue_t *kqueue = nullptr;
+    char *kargs_noop = nullptr;
+    alignas(64) std::atomic<uint64_t> last_packet_ns{0};
+    std::atomic<uint64_t> last_call_ns{0};      // the keep-alive runs for a window after this
+    std::atomic<int> call_busy{0};
+    char pad_[64 - 2 * sizeof(std::atomic<uint64_t>) - sizeof(std::atomic<int>)];
 };
 
 DevState g_dev[kMaxDirectDev];
@@ -120,6 +135,60 @@ static inline uint64_t sys_ts() {
     return t;
 }
 uint64_t g_ts_freq = 0;
+
+uint64_t mono_ns() {
+    timespec t;
+    clock_gettime(CLOCK_MONOTONIC, &t);
+    return (uint64_t)t.tv_sec * 1000000000ull + (uint64_t)t.tv_nsec;
+}
+
+// Keep-alive: after 50-100 us without a packet the command processor drops
+// into a deeper idle state and the next doorbell takes ~10 us instead of ~5 to
+// start the kernel (tools/idle_gap_probe.py: a 4 MiB call 9.6 us after a 50 us
+// host gap, 14.9-15.5 us after 100 us-5 ms), which every combine step of a
+// schedule that waits on the network would pay.  A kernel in flight on another
+// queue does not prevent it (tools/idle_sleep_probe.py): it is the CP's
+// doorbell handling that sleeps.  With MPIR_CVAR_REDUCE_LOCAL_KEEPALIVE_US = P
+// (40 is the measured choice; default 0 = off), while the direct path has been
+// used in the last MPIR_CVAR_REDUCE_LOCAL_KEEPALIVE_MS (default 20), a library
+// thread puts an empty barrier-AND packet on a queue of its own whenever no
+// packet has gone for P us: the same calls then take 9.4-10.3 us after any
+// gap (tools/keepalive_ab.sh, profiles/r02/keepalive_ab.log).  It is off by
+// default because its wake-ups cost back-to-back callers 0-1 % in alternated
+// A/Bs (tools/keepalive_headline_ab.sh, profiles/r02/keepalive_headline_ab.log).
+// _KIND=kernel (one workgroup of the SUM tile kernel with nothing to do) and
+// _QUEUE=same (the calls' queue) are the A/B's other variants, no better.
+// Idle for longer than the window, the thread naps 1 ms at a time.
+int keepalive_us() {
+    static const int v = [] {
+        const char *e = getenv("MPIR_CVAR_REDUCE_LOCAL_KEEPALIVE_US");
+        const int us = e ? atoi(e) : 0;
+        return us > 0 && us <= 100000 ? us : 0;
+    }();
+    return v;
+}
+int keepalive_kernel() {
+    static const int v = [] {
+        const char *e = getenv("MPIR_CVAR_REDUCE_LOCAL_KEEPALIVE_KIND");
+        return (e && !strcmp(e, "kernel")) ? 1 : 0;
+    }();
+    return v;
+}
+int keepalive_own_queue() {
+    static const int v = [] {
+        const char *e = getenv("MPIR_CVAR_REDUCE_LOCAL_KEEPALIVE_QUEUE");
+        return (e && !strcmp(e, "same")) ? 0 : 1;
+    }();
+    return v;
+}
+uint64_t keepalive_active_ns() {
+    static const uint64_t v = [] {
+        const char *e = getenv("MPIR_CVAR_REDUCE_LOCAL_KEEPALIVE_MS");
+        const long ms = e ? atol(e) : 20;
+        return (uint64_t)(ms > 0 && ms <= 60000 ? ms : 20) * 1000000ull;
+    }();
+    return v;
+}
 
 int mode() {
     static const int m = [] {
@@ -361,8 +430,127 @@ void init_dev(int dev, DevState &d) {
     if (!g_ts_freq) hsa_system_get_info(HSA_SYSTEM_INFO_TIMESTAMP_FREQUENCY, &g_ts_freq);
     d.karg = static_cast<char *>(kp);
     d.hdp = hdp.HDP_MEM_FLUSH_CNTL;
+    if (keepalive_us()) {
+        void *na = nullptr;
+        if (hsa_amd_memory_pool_allocate(f.vram, 256, 0, &na) == HSA_STATUS_SUCCESS &&
+            hsa_amd_agents_allow_access(1, &f.cpu, nullptr, na) == HSA_STATUS_SUCCESS) {
+            memset(na, 0, 256);      // LeanArgs {in, io, vbytes = 0, keep}: every workgroup returns at once
+            _mm_sfence();
+            *d.hdp = 1u;
+            (void)*d.hdp;
+            d.kargs_noop = static_cast<char *>(na);
+        }
+        if (keepalive_own_queue() &&
+            hsa_queue_create(f.gpu, 64, HSA_QUEUE_TYPE_MULTI, queue_error_cb, &d, UINT32_MAX, UINT32_MAX,
+                             &d.kqueue) != HSA_STATUS_SUCCESS)
+            d.kqueue = nullptr;
+        if (!keepalive_own_queue()) d.kqueue = d.queue;
+    }
     d.ok = true;
     d.state = 1;
+}
+
+// ---- keep-alive thread (keepalive_us()) --------------------------------------
+std::atomic<bool> g_keepalive_stop{false};
+std::once_flag g_keepalive_once;
+
+// one no-op packet on d.kqueue, no completion signal (under d.publish)
+void keepalive_packet(DevState &d) {
+    hsa_queue_t *q = d.kqueue;
+    const uint64_t idx = hsa_queue_load_write_index_relaxed(q);
+    if (idx - hsa_queue_load_read_index_scacquire(q) >= q->size) return;   // full: the CP is busy anyway
+    const uint64_t ko = d.kobj[0][MPIR_HIP_OP_SUM][MPIR_HIP_F32];
+    uint16_t header;
+    uint16_t setup = 0;
+    if (keepalive_kernel() && ko && d.kargs_noop) {
+        hsa_kernel_dispatch_packet_t *p = (hsa_kernel_dispatch_packet_t *)q->base_address + (idx & (q->size - 1));
+        memset((char *)p + 4, 0, sizeof(*p) - 4);
+        p->workgroup_size_x = kThreads;
+        p->workgroup_size_y = 1;
+        p->workgroup_size_z = 1;
+        p->grid_size_x = kThreads;
+        p->grid_size_y = 1;
+        p->grid_size_z = 1;
+        p->kernel_object = ko;
+        p->kernarg_address = d.kargs_noop;
+        header = (HSA_PACKET_TYPE_KERNEL_DISPATCH << HSA_PACKET_HEADER_TYPE) |
+                 (HSA_FENCE_SCOPE_NONE << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE) |
+                 (HSA_FENCE_SCOPE_NONE << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE);
+        setup = 1 << HSA_KERNEL_DISPATCH_PACKET_SETUP_DIMENSIONS;
+    } else {
+        hsa_barrier_and_packet_t *p = (hsa_barrier_and_packet_t *)q->base_address + (idx & (q->size - 1));
+        memset((char *)p + 4, 0, sizeof(*p) - 4);
+        header = (HSA_PACKET_TYPE_BARRIER_AND << HSA_PACKET_HEADER_TYPE) |
+                 (HSA_FENCE_SCOPE_NONE << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE) |
+                 (HSA_FENCE_SCOPE_NONE << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE);
+    }
+    hsa_queue_store_write_index_relaxed(q, idx + 1);
+    _mm_sfence();
+    __atomic_store_n((uint32_t *)((char *)q->base_address + (idx & (q->size - 1)) * 64),
+                     (uint32_t)header | ((uint32_t)setup << 16), __ATOMIC_RELEASE);
+    hsa_signal_store_screlease(q->doorbell_signal, idx);
+}
+
+void keepalive_loop() {
+    prctl(PR_SET_TIMERSLACK, 1000UL);     // 1 us: nanosleep wakes near the period
+    // SCHED_IDLE: the thread runs on otherwise idle cores only and never
+    // preempts the callers' threads (with the default policy its wake-ups cost
+    // back-to-back 64 MiB callers ~1 %, profiles/r02/keepalive_headline_ab.log)
+    sched_param sp{};
+    sp.sched_priority = 0;
+    (void)pthread_setschedparam(pthread_self(), SCHED_IDLE, &sp);
+    const uint64_t period = (uint64_t)keepalive_us() * 1000ull;
+    // naps: half a period while some device idles inside its window (a packet
+    // goes out at most 1.5 periods after the last one), a whole period while a
+    // call is in flight (the CP is busy; fewer wake-ups for back-to-back
+    // callers), 1 ms once every window has expired
+    const timespec nap = {0, (long)(period / 2)}, busy_nap = {0, (long)period}, idle_nap = {0, 1000000};
+    int state = 1;    // 0 nothing in its window, 1 idle in its window, 2 a call in flight
+    while (!g_keepalive_stop.load(std::memory_order_relaxed)) {
+        nanosleep(state == 0 ? &idle_nap : state == 2 ? &busy_nap : &nap, nullptr);
+        const uint64_t t = mono_ns();
+        bool active = false, busy = false;
+        for (int i = 0; i < kMaxDirectDev; ++i) {
+            DevState &d = g_dev[i];
+            if (!d.ok || !d.kqueue || d.queue_error.load(std::memory_order_relaxed)) continue;
+            // (signed: a call may have stamped a time after this thread read the clock)
+            const uint64_t lc = d.last_call_ns.load(std::memory_order_relaxed);
+            if (!lc || (int64_t)(t - lc) > (int64_t)keepalive_active_ns()) continue;
+            active = true;
+            const uint64_t last = d.last_packet_ns.load(std::memory_order_relaxed);
+            if (d.call_busy.load(std::memory_order_relaxed)) {
+                busy = true;
+                continue;
+            }
+            if ((int64_t)(t - last) < (int64_t)period) continue;
+            std::lock_guard<std::mutex> lk(d.publish);
+            if (g_keepalive_stop.load(std::memory_order_relaxed)) return;
+            // re-check under the lock: a call that published meanwhile is in flight
+            if (d.call_busy.load(std::memory_order_relaxed) ||
+                (int64_t)(mono_ns() - d.last_packet_ns.load(std::memory_order_relaxed)) < (int64_t)period)
+                continue;
+            keepalive_packet(d);
+            d.last_packet_ns.store(mono_ns(), std::memory_order_relaxed);
+        }
+        state = !active ? 0 : busy ? 2 : 1;
+    }
+}
+
+// at exit, before the HIP / HSA runtimes tear down (registered after they
+// initialised, so it runs first): no packet after this returns
+void keepalive_stop() {
+    g_keepalive_stop.store(true);
+    for (int i = 0; i < kMaxDirectDev; ++i) {
+        if (!g_dev[i].ok) continue;
+        std::lock_guard<std::mutex> lk(g_dev[i].publish);
+    }
+}
+
+void keepalive_start() {
+    std::call_once(g_keepalive_once, [] {
+        atexit(keepalive_stop);
+        std::thread(keepalive_loop).detach();
+    });
 }
 
 }  // namespace
@@ -422,6 +610,7 @@ int direct_reduce(int dev, int op, int elem, const ReducePlan &p, int *rc) {
     DevState &d = g_dev[dev];
     std::call_once(d.once, [&] { init_dev(dev, d); });
     if (!d.ok || d.queue_error.load(std::memory_order_relaxed)) return 0;
+    if (keepalive_us()) keepalive_start();
     const uint64_t ko = d.kobj[p.kind][op][elem];
     // the packet's grid_size_x (workgroups x kThreads) is 32 bits
     if (!ko || p.groups == 0 || p.groups > (uint64_t)UINT32_MAX / kThreads) return 0;
@@ -515,6 +704,7 @@ int direct_reduce(int dev, int op, int elem, const ReducePlan &p, int *rc) {
         __atomic_store_n((uint32_t *)p, (uint32_t)header | ((uint32_t)setup << 16), __ATOMIC_RELEASE);
         if (prof) th1 = sys_ts();
         hsa_signal_store_screlease(q->doorbell_signal, idx);
+        if (keepalive_us()) d.call_busy.store(1, std::memory_order_relaxed);
     }
     for (uint64_t it = 1; hsa_signal_load_scacquire(sig) != 0; ++it) {
         if ((it & 0xFFFF) == 0 && d.queue_error.load(std::memory_order_relaxed)) {
@@ -525,6 +715,14 @@ int direct_reduce(int dev, int op, int elem, const ReducePlan &p, int *rc) {
     }
     if (held) held->inflight.fetch_sub(1, std::memory_order_acq_rel);
     if (ring >= 0) d.ring_busy[ring].store(0, std::memory_order_release);
+    if (keepalive_us()) {
+        // (with several threads calling, one's end may clear another's busy
+        // flag: at worst a keep-alive packet goes out during a call, harmless)
+        const uint64_t t = mono_ns();
+        d.last_packet_ns.store(t, std::memory_order_relaxed);
+        d.last_call_ns.store(t, std::memory_order_relaxed);
+        d.call_busy.store(0, std::memory_order_relaxed);
+    }
     if (prof) {
         const uint64_t th2 = sys_ts();
         hsa_amd_profiling_dispatch_time_t t{};
