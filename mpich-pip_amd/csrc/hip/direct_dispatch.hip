@@ -97,6 +97,7 @@ struct DevState {
     hsa_agent_t agent{};
     hsa_queue_t *queue = nullptr;               // the calls' queue (no dispatch timestamps)
     hsa_queue_t *pqueue = nullptr;              // the same, timestamps on: calls while profiling is on
+    std::once_flag ponce;                       // (created at the first profiled call)
     char *karg = nullptr;                       // kKargSlots x kKargSlotBytes, VRAM, host-written
     uint32_t kslot = 0;                         // next ring slot to try (under `publish`)
     std::atomic<int> ring_busy[kRingSlots] = {};  // a ring slot's dispatch is in flight
@@ -109,12 +110,15 @@ struct DevState {
     // their own, the monotonic time of the last call's end or keep-alive packet
     // and whether a call is in flight (a busy CP is not idle: no keep-alive
     // then).  Plain stores on the call path, no read-modify-write.
-    hsa_queue_t *kqueue = nullptr;
+    hsa_queue_t *kqueue = nullptr;              // created when the keep-alive is first armed
+    std::once_flag konce;
+    std::atomic<bool> kready{false};
     char *kargs_noop = nullptr;
     alignas(64) std::atomic<uint64_t> last_packet_ns{0};
     std::atomic<uint64_t> last_call_ns{0};      // the keep-alive runs for a window after this
     std::atomic<int> call_busy{0};
-    char pad_[64 - 2 * sizeof(std::atomic<uint64_t>) - sizeof(std::atomic<int>)];
+    std::atomic<int> armed{0};                  // the caller has been seen to leave gaps
+    char pad_[64 - 2 * sizeof(std::atomic<uint64_t>) - 2 * sizeof(std::atomic<int>)];
 };
 
 DevState g_dev[kMaxDirectDev];
@@ -148,14 +152,20 @@ uint64_t mono_ns() {
 // host gap, 14.9-15.5 us after 100 us-5 ms), which every combine step of a
 // schedule that waits on the network would pay.  A kernel in flight on another
 // queue does not prevent it (tools/idle_sleep_probe.py): it is the CP's
-// doorbell handling that sleeps.  With MPIR_CVAR_REDUCE_LOCAL_KEEPALIVE_US = P
-// (40 is the measured choice; default 0 = off), while the direct path has been
-// used in the last MPIR_CVAR_REDUCE_LOCAL_KEEPALIVE_MS (default 20), a library
-// thread puts an empty barrier-AND packet on a queue of its own whenever no
-// packet has gone for P us: the same calls then take 9.4-10.3 us after any
-// gap (tools/keepalive_ab.sh, profiles/r02/keepalive_ab.log).  It is off by
-// default because its wake-ups cost back-to-back callers 0-1 % in alternated
-// A/Bs (tools/keepalive_headline_ab.sh, profiles/r02/keepalive_headline_ab.log).
+// doorbell handling that sleeps.  MPIR_CVAR_REDUCE_LOCAL_KEEPALIVE_US = P
+// (opt-in, e.g. 40; default 0 = off): a call that arrives more than P + 10 us
+// after the previous one ends arms the keep-alive, one that arrives within P us
+// disarms it; while armed and within MPIR_CVAR_REDUCE_LOCAL_KEEPALIVE_MS
+// (default 20) of the last call, a library thread puts an empty barrier-AND
+// packet on a queue of its own whenever no packet has gone for P us.  Sparse
+// callers then take 9.4-10.3 us after any gap instead of ~15
+// (tools/keepalive_ab.sh, profiles/r02/keepalive_ab.log).  It stays opt-in:
+// while the thread is active some calls that meet its packets take ~18 us
+// longer (tools/ka_probe.py, profiles/r02/ka_probe.log), and in alternated A/Bs
+// of back-to-back loops it cost 0-1 % (always-on thread) or, armed by the
+// bench's own pauses, much more (tools/keepalive_headline_ab.sh,
+// tools/lazy_queues_ab.sh, profiles/r02/keepalive_headline_ab.log,
+// lazy_queues_ab.log).  Not understood yet; next round.
 // _KIND=kernel (one workgroup of the SUM tile kernel with nothing to do) and
 // _QUEUE=same (the calls' queue) are the A/B's other variants, no better.
 // Idle for longer than the window, the thread naps 1 ms at a time.
@@ -417,16 +427,15 @@ void init_dev(int dev, DevState &d) {
         hsa_amd_memory_pool_free(kp);
         return;
     }
-    if (hsa_queue_create(f.gpu, kQueueSize, HSA_QUEUE_TYPE_MULTI, queue_error_cb, &d, UINT32_MAX, UINT32_MAX,
-                         &d.pqueue) != HSA_STATUS_SUCCESS) {
-        hsa_queue_destroy(d.queue);
-        hsa_amd_memory_pool_free(kp);
-        return;
-    }
     d.agent = f.gpu;
-    // timestamps on from creation (see timestamps())
-    hsa_amd_profiling_set_profiler_enabled(d.pqueue, 1);
     if (timestamps()) hsa_amd_profiling_set_profiler_enabled(d.queue, 1);
+    // A/B only (tools/lazy_queues_ab.sh): idle queues that exist and are never used
+    if (const char *xq = getenv("MPIR_CVAR_REDUCE_LOCAL_DIRECT_IDLE_QUEUES")) {
+        for (int k = atoi(xq); k > 0 && k <= 8; --k) {
+            hsa_queue_t *q = nullptr;
+            (void)hsa_queue_create(f.gpu, 64, HSA_QUEUE_TYPE_MULTI, nullptr, nullptr, UINT32_MAX, UINT32_MAX, &q);
+        }
+    }
     if (!g_ts_freq) hsa_system_get_info(HSA_SYSTEM_INFO_TIMESTAMP_FREQUENCY, &g_ts_freq);
     d.karg = static_cast<char *>(kp);
     d.hdp = hdp.HDP_MEM_FLUSH_CNTL;
@@ -440,14 +449,38 @@ void init_dev(int dev, DevState &d) {
             (void)*d.hdp;
             d.kargs_noop = static_cast<char *>(na);
         }
-        if (keepalive_own_queue() &&
-            hsa_queue_create(f.gpu, 64, HSA_QUEUE_TYPE_MULTI, queue_error_cb, &d, UINT32_MAX, UINT32_MAX,
-                             &d.kqueue) != HSA_STATUS_SUCCESS)
-            d.kqueue = nullptr;
-        if (!keepalive_own_queue()) d.kqueue = d.queue;
     }
     d.ok = true;
     d.state = 1;
+}
+
+// Every extra queue is created only when first needed: an idle queue that
+// merely exists costs the calls' queue ~1 % at 64 MiB (the CP has one more
+// queue to serve; profiles/r02/keepalive_headline_ab.log, lazy_queues_ab.log).
+hsa_queue_t *profiled_queue(DevState &d) {
+    std::call_once(d.ponce, [&] {
+        hsa_queue_t *q = nullptr;
+        if (hsa_queue_create(d.agent, kQueueSize, HSA_QUEUE_TYPE_MULTI, queue_error_cb, &d, UINT32_MAX, UINT32_MAX,
+                             &q) != HSA_STATUS_SUCCESS)
+            return;
+        // timestamps on from creation (see timestamps())
+        hsa_amd_profiling_set_profiler_enabled(q, 1);
+        d.pqueue = q;
+    });
+    return d.pqueue ? d.pqueue : d.queue;
+}
+
+bool keepalive_queue(DevState &d) {
+    std::call_once(d.konce, [&] {
+        if (!keepalive_own_queue()) {
+            d.kqueue = d.queue;
+        } else if (hsa_queue_create(d.agent, 64, HSA_QUEUE_TYPE_MULTI, queue_error_cb, &d, UINT32_MAX, UINT32_MAX,
+                                    &d.kqueue) != HSA_STATUS_SUCCESS) {
+            d.kqueue = nullptr;
+        }
+        d.kready.store(d.kqueue != nullptr);
+    });
+    return d.kready.load();
 }
 
 // ---- keep-alive thread (keepalive_us()) --------------------------------------
@@ -512,10 +545,12 @@ void keepalive_loop() {
         bool active = false, busy = false;
         for (int i = 0; i < kMaxDirectDev; ++i) {
             DevState &d = g_dev[i];
-            if (!d.ok || !d.kqueue || d.queue_error.load(std::memory_order_relaxed)) continue;
+            if (!d.ok || !d.kready.load(std::memory_order_acquire) || d.queue_error.load(std::memory_order_relaxed))
+                continue;
             // (signed: a call may have stamped a time after this thread read the clock)
             const uint64_t lc = d.last_call_ns.load(std::memory_order_relaxed);
-            if (!lc || (int64_t)(t - lc) > (int64_t)keepalive_active_ns()) continue;
+            if (!d.armed.load(std::memory_order_relaxed) || !lc || (int64_t)(t - lc) > (int64_t)keepalive_active_ns())
+                continue;
             active = true;
             const uint64_t last = d.last_packet_ns.load(std::memory_order_relaxed);
             if (d.call_busy.load(std::memory_order_relaxed)) {
@@ -610,7 +645,22 @@ int direct_reduce(int dev, int op, int elem, const ReducePlan &p, int *rc) {
     DevState &d = g_dev[dev];
     std::call_once(d.once, [&] { init_dev(dev, d); });
     if (!d.ok || d.queue_error.load(std::memory_order_relaxed)) return 0;
-    if (keepalive_us()) keepalive_start();
+    if (keepalive_us()) {
+        // arm on a call after a gap, disarm on a back-to-back one
+        const uint64_t lc = d.last_call_ns.load(std::memory_order_relaxed);
+        if (lc) {
+            const int64_t gap = (int64_t)(mono_ns() - lc);
+            const int64_t p = (int64_t)keepalive_us() * 1000;
+            if (gap > p + 10000) {
+                if (!d.armed.load(std::memory_order_relaxed) && keepalive_queue(d)) {
+                    d.armed.store(1, std::memory_order_relaxed);
+                    keepalive_start();
+                }
+            } else if (gap < p && d.armed.load(std::memory_order_relaxed)) {
+                d.armed.store(0, std::memory_order_relaxed);
+            }
+        }
+    }
     const uint64_t ko = d.kobj[p.kind][op][elem];
     // the packet's grid_size_x (workgroups x kThreads) is 32 bits
     if (!ko || p.groups == 0 || p.groups > (uint64_t)UINT32_MAX / kThreads) return 0;
@@ -679,7 +729,7 @@ int direct_reduce(int dev, int op, int elem, const ReducePlan &p, int *rc) {
             *d.hdp = 1u;        // HDP flush: the BAR writes land in VRAM before the CP reads them
             (void)*d.hdp;
         }
-        hsa_queue_t *q = prof ? d.pqueue : d.queue;
+        hsa_queue_t *q = prof ? profiled_queue(d) : d.queue;
         const uint64_t idx = hsa_queue_load_write_index_relaxed(q);
         while (idx - hsa_queue_load_read_index_scacquire(q) >= q->size) _mm_pause();
         hsa_kernel_dispatch_packet_t *p = (hsa_kernel_dispatch_packet_t *)q->base_address + (idx & (q->size - 1));
