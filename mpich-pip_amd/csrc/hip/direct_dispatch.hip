@@ -153,19 +153,18 @@ uint64_t mono_ns() {
 // schedule that waits on the network would pay.  A kernel in flight on another
 // queue does not prevent it (tools/idle_sleep_probe.py): it is the CP's
 // doorbell handling that sleeps.  MPIR_CVAR_REDUCE_LOCAL_KEEPALIVE_US = P
-// (opt-in, e.g. 40; default 0 = off): a call that arrives more than P + 10 us
-// after the previous one ends arms the keep-alive, one that arrives within P us
-// disarms it; while armed and within MPIR_CVAR_REDUCE_LOCAL_KEEPALIVE_MS
-// (default 20) of the last call, a library thread puts an empty barrier-AND
-// packet on a queue of its own whenever no packet has gone for P us.  Sparse
-// callers then take 9.4-10.3 us after any gap instead of ~15
-// (tools/keepalive_ab.sh, profiles/r02/keepalive_ab.log).  It stays opt-in:
-// while the thread is active some calls that meet its packets take ~18 us
-// longer (tools/ka_probe.py, profiles/r02/ka_probe.log), and in alternated A/Bs
-// of back-to-back loops it cost 0-1 % (always-on thread) or, armed by the
-// bench's own pauses, much more (tools/keepalive_headline_ab.sh,
-// tools/lazy_queues_ab.sh, profiles/r02/keepalive_headline_ab.log,
-// lazy_queues_ab.log).  Not understood yet; next round.
+// (opt-in, e.g. 40; default 0 = off -- with it on, bench.py's back-to-back loop
+// measured 0.763-0.786 against 0.79-0.80: profiles/r02/keepalive_default_bench.log): a call that arrives more than P + 10 us after the
+// previous one ends arms the keep-alive, one that arrives within P us disarms
+// it; while armed and within MPIR_CVAR_REDUCE_LOCAL_KEEPALIVE_MS (default 20)
+// of the last call, a library thread puts an empty barrier-AND packet on the
+// calls' own queue whenever no packet has gone for P us and no call is in
+// flight.  Sparse callers then take ~10 us after any gap instead of ~15, with
+// no slow outliers and no cost to back-to-back loops
+// (tools/keepalive_same_ab.sh, profiles/r02/keepalive_same_ab.log).  On a queue
+// of its own (_QUEUE=own) the packets made the hardware scheduler map one more
+// active queue: calls that met them took ~18 us longer (tools/ka_probe.py,
+// profiles/r02/ka_probe.log, keepalive_headline_ab.log, lazy_queues_ab.log).
 // _KIND=kernel (one workgroup of the SUM tile kernel with nothing to do) and
 // _QUEUE=same (the calls' queue) are the A/B's other variants, no better.
 // Idle for longer than the window, the thread naps 1 ms at a time.
@@ -187,7 +186,7 @@ int keepalive_kernel() {
 int keepalive_own_queue() {
     static const int v = [] {
         const char *e = getenv("MPIR_CVAR_REDUCE_LOCAL_KEEPALIVE_QUEUE");
-        return (e && !strcmp(e, "same")) ? 0 : 1;
+        return (e && !strcmp(e, "own")) ? 1 : 0;
     }();
     return v;
 }
@@ -485,6 +484,7 @@ bool keepalive_queue(DevState &d) {
 
 // ---- keep-alive thread (keepalive_us()) --------------------------------------
 std::atomic<bool> g_keepalive_stop{false};
+std::atomic<uint64_t> g_keepalive_packets{0}, g_keepalive_arms{0};
 std::once_flag g_keepalive_once;
 
 // one no-op packet on d.kqueue, no completion signal (under d.publish)
@@ -565,6 +565,7 @@ void keepalive_loop() {
                 (int64_t)(mono_ns() - d.last_packet_ns.load(std::memory_order_relaxed)) < (int64_t)period)
                 continue;
             keepalive_packet(d);
+            g_keepalive_packets.fetch_add(1, std::memory_order_relaxed);
             d.last_packet_ns.store(mono_ns(), std::memory_order_relaxed);
         }
         state = !active ? 0 : busy ? 2 : 1;
@@ -575,6 +576,9 @@ void keepalive_loop() {
 // initialised, so it runs first): no packet after this returns
 void keepalive_stop() {
     g_keepalive_stop.store(true);
+    if (getenv("MPIR_CVAR_REDUCE_LOCAL_KEEPALIVE_DEBUG"))
+        fprintf(stderr, "mpir_hip keep-alive: %llu arms, %llu packets\n",
+                (unsigned long long)g_keepalive_arms.load(), (unsigned long long)g_keepalive_packets.load());
     for (int i = 0; i < kMaxDirectDev; ++i) {
         if (!g_dev[i].ok) continue;
         std::lock_guard<std::mutex> lk(g_dev[i].publish);
@@ -654,6 +658,7 @@ int direct_reduce(int dev, int op, int elem, const ReducePlan &p, int *rc) {
             if (gap > p + 10000) {
                 if (!d.armed.load(std::memory_order_relaxed) && keepalive_queue(d)) {
                     d.armed.store(1, std::memory_order_relaxed);
+                    g_keepalive_arms.fetch_add(1, std::memory_order_relaxed);
                     keepalive_start();
                 }
             } else if (gap < p && d.armed.load(std::memory_order_relaxed)) {
