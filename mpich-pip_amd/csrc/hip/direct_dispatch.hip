@@ -586,6 +586,7 @@ void keepalive_stop() {
 }
 
 void keepalive_start() {
+    if (getenv("MPIR_CVAR_REDUCE_LOCAL_KEEPALIVE_NOTHREAD")) return;   // A/B only
     std::call_once(g_keepalive_once, [] {
         atexit(keepalive_stop);
         std::thread(keepalive_loop).detach();
