@@ -526,12 +526,8 @@ void keepalive_packet(DevState &d) {
 
 void keepalive_loop() {
     prctl(PR_SET_TIMERSLACK, 1000UL);     // 1 us: nanosleep wakes near the period
-    // SCHED_IDLE: the thread runs on otherwise idle cores only and never
-    // preempts the callers' threads (with the default policy its wake-ups cost
-    // back-to-back 64 MiB callers ~1 %, profiles/r02/keepalive_headline_ab.log)
-    sched_param sp{};
-    sp.sched_priority = 0;
-    (void)pthread_setschedparam(pthread_self(), SCHED_IDLE, &sp);
+    // (no SCHED_IDLE: with it, the napping thread alone cost bench.py's
+    // spinning caller 4-21 %, profiles/r02/ka_isolate.log)
     const uint64_t period = (uint64_t)keepalive_us() * 1000ull;
     // naps: half a period while some device idles inside its window (a packet
     // goes out at most 1.5 periods after the last one), a whole period while a
