@@ -525,6 +525,11 @@ void keepalive_packet(DevState &d) {
 }
 
 void keepalive_loop() {
+    if (getenv("MPIR_CVAR_REDUCE_LOCAL_KEEPALIVE_EMPTY")) {   // A/B only: a thread that only naps
+        const timespec ms = {0, 1000000};
+        while (!g_keepalive_stop.load(std::memory_order_relaxed)) nanosleep(&ms, nullptr);
+        return;
+    }
     prctl(PR_SET_TIMERSLACK, 1000UL);     // 1 us: nanosleep wakes near the period
     // (no SCHED_IDLE: with it, the napping thread alone cost bench.py's
     // spinning caller 4-21 %, profiles/r02/ka_isolate.log)
