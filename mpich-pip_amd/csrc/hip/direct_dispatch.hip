@@ -524,7 +524,25 @@ void keepalive_packet(DevState &d) {
     hsa_signal_store_screlease(q->doorbell_signal, idx);
 }
 
-void keepalive_loop() {
+// Keep the thread off the caller's core: pin it to the highest-numbered CPU of
+// its affinity mask other than the one the arming call ran on (a napping thread
+// free to share the spinning caller's core cost it 2-6 %, ka_isolate.log).
+void keepalive_pin(int caller_cpu) {
+    if (getenv("MPIR_CVAR_REDUCE_LOCAL_KEEPALIVE_NOPIN")) return;   // A/B only
+    cpu_set_t set;
+    if (sched_getaffinity(0, sizeof set, &set) != 0) return;
+    for (int c = CPU_SETSIZE - 1; c >= 0; --c) {
+        if (c == caller_cpu || !CPU_ISSET(c, &set)) continue;
+        cpu_set_t one;
+        CPU_ZERO(&one);
+        CPU_SET(c, &one);
+        (void)pthread_setaffinity_np(pthread_self(), sizeof one, &one);
+        return;
+    }
+}
+
+void keepalive_loop(int caller_cpu) {
+    keepalive_pin(caller_cpu);
     if (getenv("MPIR_CVAR_REDUCE_LOCAL_KEEPALIVE_EMPTY")) {   // A/B only: a thread that only naps
         const timespec ms = {0, 1000000};
         while (!g_keepalive_stop.load(std::memory_order_relaxed)) nanosleep(&ms, nullptr);
@@ -590,7 +608,7 @@ void keepalive_start() {
     if (getenv("MPIR_CVAR_REDUCE_LOCAL_KEEPALIVE_NOTHREAD")) return;   // A/B only
     std::call_once(g_keepalive_once, [] {
         atexit(keepalive_stop);
-        std::thread(keepalive_loop).detach();
+        std::thread(keepalive_loop, sched_getcpu()).detach();
     });
 }
 
