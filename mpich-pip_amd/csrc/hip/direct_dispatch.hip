@@ -40,6 +40,7 @@
 #include <hip/hip_runtime.h>
 #include <hsa/hsa.h>
 #include <hsa/hsa_ext_amd.h>
+#include <hsa/amd_hsa_signal.h>
 #include <dlfcn.h>
 #include <immintrin.h>
 #include <stdio.h>
@@ -139,6 +140,33 @@ static inline uint64_t sys_ts() {
     return t;
 }
 uint64_t g_ts_freq = 0;
+
+// MPIR_CVAR_REDUCE_LOCAL_WAIT_MWAITX=1 (A/B, AMD hosts with MONITORX): wait for
+// the completion signal's value line with MONITORX / MWAITX instead of a
+// pause loop (tools/mwaitx_ab.sh)
+bool use_mwaitx() {
+    static const bool v = [] {
+        const char *e = getenv("MPIR_CVAR_REDUCE_LOCAL_WAIT_MWAITX");
+        if (!e || atoi(e) == 0) return false;
+        unsigned a, b, c, dd;
+        __asm__ volatile("cpuid" : "=a"(a), "=b"(b), "=c"(c), "=d"(dd) : "a"(0x80000001u), "c"(0));
+        return ((c >> 29) & 1u) != 0;   // CPUID Fn8000_0001 ECX[29] = MONITORX
+    }();
+    return v;
+}
+
+__attribute__((target("mwaitx"))) void wait_signal_mwaitx(hsa_signal_t sig) {
+#if !defined(__HIP_DEVICE_COMPILE__)     // host code; the device pass never emits it
+    volatile int64_t *v = &reinterpret_cast<amd_signal_t *>(sig.handle)->value;
+    while (__atomic_load_n(v, __ATOMIC_ACQUIRE) != 0) {
+        __builtin_ia32_monitorx((void *)v, 0, 0);
+        if (__atomic_load_n(v, __ATOMIC_ACQUIRE) == 0) break;
+        __builtin_ia32_mwaitx(0x2, 0, 20000);   // ECX bit 1: EBX timer, at most ~20000 TSC ticks
+    }
+#else
+    (void)sig;
+#endif
+}
 
 uint64_t mono_ns() {
     timespec t;
@@ -781,6 +809,7 @@ int direct_reduce(int dev, int op, int elem, const ReducePlan &p, int *rc) {
         hsa_signal_store_screlease(q->doorbell_signal, idx);
         if (keepalive_us()) d.call_busy.store(1, std::memory_order_relaxed);
     }
+    if (use_mwaitx() && !d.queue_error.load(std::memory_order_relaxed)) wait_signal_mwaitx(sig);
     for (uint64_t it = 1; hsa_signal_load_scacquire(sig) != 0; ++it) {
         if ((it & 0xFFFF) == 0 && d.queue_error.load(std::memory_order_relaxed)) {
             *rc = MPIR_HIP_ERUNTIME;
