@@ -343,7 +343,10 @@ CopyPool &copy_pool() {
     return *pool;
 }
 
-enum Loc { LOC_HOST = 0, LOC_DEVICE = 1 };
+// LOC_HOST: pageable (or unknown to HIP); LOC_PINNED: page-locked host memory
+// (hipHostMalloc / hipHostRegister), which DMA copies and kernels may still be
+// writing when the caller hands it over
+enum Loc { LOC_HOST = 0, LOC_DEVICE = 1, LOC_PINNED = 2 };
 
 // Both operands in host memory and at most this many bytes each: the combine
 // runs on the host (host_loop, the same functors as the kernels; split over
@@ -420,18 +423,8 @@ uint64_t host_split_bytes() {
     return v;
 }
 
-// page-locked host memory (hipHostMalloc / hipHostRegister): DMA-able as is
-bool is_pinned_host(const void *p) {
-    hipPointerAttribute_t at;
-    if (hipPointerGetAttributes(&at, p) != hipSuccess) {
-        (void)hipGetLastError();
-        return false;
-    }
-    return at.type == hipMemoryTypeHost;
-}
-
-// Device memory (hipMalloc, managed) is combined in place; anything else
-// (pageable or pinned host memory) is staged through device scratch.
+// Device memory (hipMalloc, managed) is combined in place; host memory
+// (pageable or pinned) takes the host combine, the pinned slot or staging.
 Loc classify(const void *p, int *dev) {
     hipPointerAttribute_t at;
     hipError_t e = hipPointerGetAttributes(&at, p);
@@ -443,7 +436,33 @@ Loc classify(const void *p, int *dev) {
         *dev = at.device;
         return LOC_DEVICE;
     }
-    return LOC_HOST;
+    return at.type == hipMemoryTypeHost ? LOC_PINNED : LOC_HOST;
+}
+
+// devices visible to this process (0 on a CPU-only rank: host operands are
+// still combined there, as the reference's loop runs anywhere)
+int device_count() {
+    static const int n = [] {
+        int c = 0;
+        if (hipGetDeviceCount(&c) != hipSuccess) { (void)hipGetLastError(); c = 0; }
+        return c;
+    }();
+    return n;
+}
+
+// A pinned host operand may be the target of work the caller queued on the
+// legacy null stream (a hipMemcpyAsync D2H, a kernel writing mapped memory):
+// the host reads it only after that work, the ordering the device path keeps
+// for device operands (direct_reduce) and the blocking library streams keep for
+// staged ones.  hipStreamQuery(NULL) keeps answering "not ready" for finished
+// work until the host synchronises (profiles/r02/direct_probe.log), so "not
+// ready" is followed by hipStreamSynchronize(NULL).  Pageable operands need
+// nothing: HIP's copies into pageable memory complete before they return.
+int order_after_null_stream() {
+    if (hipStreamQuery(nullptr) == hipSuccess) return MPIR_HIP_OK;
+    (void)hipGetLastError();
+    HIPCHK(hipStreamSynchronize(nullptr));
+    return MPIR_HIP_OK;
 }
 
 // How the synchronous entry points wait for their launch.
@@ -578,11 +597,7 @@ int MPIR_Hip_thread_contexts(void) {
     return g_ctx_created;
 }
 
-int MPIR_Hip_device_count(void) {
-    int n = 0;
-    if (hipGetDeviceCount(&n) != hipSuccess) { (void)hipGetLastError(); return 0; }
-    return n;
-}
+int MPIR_Hip_device_count(void) { return device_count(); }
 
 int MPIR_Hip_is_device_ptr(const void *p) {
     int dev = 0;
@@ -672,9 +687,13 @@ int MPIR_Hip_reduce(const void *inbuf, void *inoutbuf, uint64_t count, int op, i
         return device_call(dio, inbuf, inoutbuf, count, op, elem, (hipStream_t)hip_stream, sync);
     if (!sync) return MPIR_HIP_EBUFFER;  // the stream variant needs device buffers
 
-    // ---- small, both host-resident: combine on this thread --------------
-    if (lin == LOC_HOST && lio == LOC_HOST && count * esz <= host_max_bytes() && g_table[op][elem].host) {
-        if (MPIR_Hip_device_count() == 0) return MPIR_HIP_ENODEV;
+    // ---- both host-resident: combine on the host (no device needed) ------
+    if (lin != LOC_DEVICE && lio != LOC_DEVICE && (count * esz <= host_max_bytes() || device_count() == 0) &&
+        g_table[op][elem].host) {
+        if (lin == LOC_PINNED || lio == LOC_PINNED) {
+            const int rc = order_after_null_stream();
+            if (rc != MPIR_HIP_OK) return rc;
+        }
         const uint64_t n = count * esz / unit;
         if (count * esz < host_split_bytes() || copy_pool().threads() <= 1) {
             g_table[op][elem].host(inbuf, inoutbuf, n);
@@ -709,7 +728,18 @@ int MPIR_Hip_reduce(const void *inbuf, void *inoutbuf, uint64_t count, int op, i
         const int dev = lin == LOC_DEVICE ? din : dio;
         const uintptr_t adev = reinterpret_cast<uintptr_t>(lin == LOC_DEVICE ? inbuf : (const void *)inoutbuf);
         char *slot = nullptr;
-        int rc = get_zc(dev, (size_t)bytes + 256, &slot);
+        int rc = MPIR_HIP_OK;
+        if (lin == LOC_PINNED || lio == LOC_PINNED) {
+            // the host operand is read (copied into the slot) before device_call's
+            // own null-stream check: order it first
+            int cur = 0;
+            HIPCHK(hipGetDevice(&cur));
+            if (cur != dev) HIPCHK(hipSetDevice(dev));
+            rc = order_after_null_stream();
+            if (cur != dev) (void)hipSetDevice(cur);
+            if (rc != MPIR_HIP_OK) return rc;
+        }
+        rc = get_zc(dev, (size_t)bytes + 256, &slot);
         if (rc != MPIR_HIP_OK) return rc;
         slot += adev & 255;
         // host <-> slot copies: split over the copy pool from zc_split_bytes() up
@@ -736,8 +766,8 @@ int MPIR_Hip_reduce(const void *inbuf, void *inoutbuf, uint64_t count, int op, i
     if (lio == LOC_DEVICE) dev = dio;
     else if (lin == LOC_DEVICE) dev = din;
     else {
+        if (device_count() == 0) return MPIR_HIP_ENODEV;
         HIPCHK(hipGetDevice(&dev));
-        if (MPIR_Hip_device_count() == 0) return MPIR_HIP_ENODEV;
     }
     int cur = 0;
     HIPCHK(hipGetDevice(&cur));
@@ -765,8 +795,8 @@ int MPIR_Hip_reduce(const void *inbuf, void *inoutbuf, uint64_t count, int op, i
     // Pageable host operands go through pinned bounce slots that the copy pool
     // fills and drains while the GPU works on earlier chunks (HIP's own
     // pageable path uploads ~36 GB/s; pinned memory is DMA'd directly).
-    const bool bounce_in = stage_in && lin == LOC_HOST && !is_pinned_host(inbuf);
-    const bool bounce_io = stage_io && lio == LOC_HOST && !is_pinned_host(inoutbuf);
+    const bool bounce_in = stage_in && lin == LOC_HOST;
+    const bool bounce_io = stage_io && lio == LOC_HOST;
     char *bounce = nullptr;
     if (rc == MPIR_HIP_OK && (bounce_in || bounce_io))
         rc = get_bounce(dev, (size_t)(2 * nslots) * slot_bytes, &bounce);

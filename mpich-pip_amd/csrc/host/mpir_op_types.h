@@ -47,8 +47,25 @@ unsigned MPIR_Op_check_groups(int opidx);
  * its `default:` branch (op_errno = MPI_ERR_OP). */
 int MPIR_Op_resolve_elem(int opidx, MPI_Datatype datatype);
 
-/* per-thread op error slot (mpir_thread.h:61-62, reduce_local.c:51-59,107-117) */
+/* MPICH's per-thread state and critical sections, as the drop-in sees them.
+ *   MPIR_Op_errno_ptr: the per-thread op error slot (mpir_thread.h:61-62,
+ *     reduce_local.c:51-59,107-117);
+ *   MPIR_Dropin_cs_enter / _exit: GLOBAL is the section MPI_Reduce_local and
+ *     MPI_Op_create / _free / _commutative hold (reduce_local.c:162,205,
+ *     op_create.c:151-164); HANDLE the one around the op store's avail list
+ *     (mpir_handlemem.h:221-225,338-384).
+ * Standalone build: this library's own TLS slot (op_kernels.c), a mutex for
+ * HANDLE and nothing for GLOBAL (op_objects.c).  Compiled into libmpi with
+ * -DMPIR_DROPIN_IN_LIBMPI (INTEGRATION.md Option 1): csrc/host/mpich_glue.c,
+ * built against MPICH's mpiimpl.h, binds them to MPIR_Per_thread.op_errno --
+ * the slot unchanged schedules reset and read themselves -- and to
+ * MPID_THREAD_CS_ENTER / EXIT, so libmpi's inline op releases and this
+ * library's creates serialise on the same lock. */
 int *MPIR_Op_errno_ptr(void);
+#define MPIR_DROPIN_CS_GLOBAL 0
+#define MPIR_DROPIN_CS_HANDLE 1
+void MPIR_Dropin_cs_enter(int which);
+void MPIR_Dropin_cs_exit(int which);
 
 /* record a HIP runtime failure inside an op kernel (sets op_errno) */
 void MPIR_Op_report_hip_error(const char *opname, int hip_rc);

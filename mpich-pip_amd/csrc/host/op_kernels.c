@@ -154,13 +154,18 @@ int MPIR_Op_resolve_elem(int opidx, MPI_Datatype datatype)
 
 /* ------------------------------------------------------------ errors */
 
-static __thread int op_errno_slot;
 static __thread char err_detail[256];
+
+#ifndef MPIR_DROPIN_IN_LIBMPI
+/* standalone: the library's own slot (in libmpi: MPIR_Per_thread.op_errno,
+ * mpich_glue.c) */
+static __thread int op_errno_slot;
 
 int *MPIR_Op_errno_ptr(void)
 {
     return &op_errno_slot;
 }
+#endif
 
 void MPIR_Err_set_detail(const char *fmt, ...)
 {
@@ -187,7 +192,7 @@ void MPIR_Op_report_hip_error(const char *opname, int hip_rc)
     default:
         MPIR_Err_set_detail("%s: HIP runtime error: %s", opname, MPIR_Hip_error_string());
     }
-    op_errno_slot = (hip_rc == MPIR_HIP_ENOKERNEL) ? MPI_ERR_OP : MPI_ERR_OTHER;
+    *MPIR_Op_errno_ptr() = (hip_rc == MPIR_HIP_ENOKERNEL) ? MPI_ERR_OP : MPI_ERR_OTHER;
 }
 
 /* ------------------------------------------------------------ kernels */
@@ -203,7 +208,7 @@ static void op_apply(int opidx, const char *opname, void *invec, void *inoutvec,
     int rc;
     if (!elem) {
         MPIR_Err_set_detail("MPI_Op %s operation not defined for this datatype", opname);
-        op_errno_slot = MPI_ERR_OP;
+        *MPIR_Op_errno_ptr() = MPI_ERR_OP;
         return;
     }
     if (len <= 0)       /* `for (i=0; i<len; i++)` runs zero times */
@@ -267,7 +272,7 @@ void MPIR_REPLACE(void *invec, void *inoutvec, int *Len, MPI_Datatype * type)
         count = *Len > 0 ? (uint64_t) * Len * ((h >> 8) & 0xffu) : 0;
     } else {
         MPIR_Err_set_detail("MPI_REPLACE: derived datatypes are not supported by this library");
-        op_errno_slot = MPI_ERR_TYPE;
+        *MPIR_Op_errno_ptr() = MPI_ERR_TYPE;
         return;
     }
     if (count == 0)

@@ -12,7 +12,13 @@
  * each object when its block is set up, indirect blocks of
  * MPIR_HANDLE_NUM_INDICES objects in a table of MPIR_HANDLE_NUM_BLOCKS --
  * because unchanged MPICH code walks it with inline macros (MPIR_Getb_ptr,
- * MPIR_Handle_obj_free).  A mutex stands in for MPICH's POBJ handle mutex.
+ * MPIR_Handle_obj_free).  The avail list is guarded by the HANDLE section
+ * and the MPI entry points (reduce_local.c) hold the GLOBAL one, as
+ * MPIR_Handle_obj_alloc / _free and MPI_Op_create / _free do
+ * (mpir_handlemem.h:221-225,338-384, op_create.c:151-164, op_free.c:86,120).
+ * Standalone, HANDLE is this library's mutex and GLOBAL has nothing to guard;
+ * compiled into libmpi (-DMPIR_DROPIN_IN_LIBMPI) both are MPICH's own
+ * critical sections (mpich_glue.c), the ones libmpi's inline op releases take.
  */
 #include <pthread.h>
 #include <stdlib.h>
@@ -26,7 +32,21 @@ MPIR_Object_alloc_t MPIR_Op_mem = { 0, 0, 0, 0, MPIR_OP_OBJ_KIND, sizeof(MPIR_Op
     MPIR_OP_PREALLOC
 };
 
+#ifndef MPIR_DROPIN_IN_LIBMPI
 static pthread_mutex_t op_mem_lock = PTHREAD_MUTEX_INITIALIZER;
+
+void MPIR_Dropin_cs_enter(int which)
+{
+    if (which == MPIR_DROPIN_CS_HANDLE)
+        pthread_mutex_lock(&op_mem_lock);
+}
+
+void MPIR_Dropin_cs_exit(int which)
+{
+    if (which == MPIR_DROPIN_CS_HANDLE)
+        pthread_mutex_unlock(&op_mem_lock);
+}
+#endif
 
 static unsigned make_handle(unsigned kind, unsigned bits)
 {
@@ -121,12 +141,12 @@ MPIR_Op *MPIR_Op_get_ptr_fn(MPI_Op op)
             MPIR_Op *p = NULL;
             if (MPIR_HANDLE_GET_MPI_KIND(a) != (unsigned) MPIR_Op_mem.kind)
                 return NULL;
-            pthread_mutex_lock(&op_mem_lock);
+            MPIR_Dropin_cs_enter(MPIR_DROPIN_CS_HANDLE);
             if ((int) MPIR_HANDLE_BLOCK(a) < MPIR_Op_mem.indirect_size &&
                 MPIR_HANDLE_BLOCK_INDEX(a) < MPIR_HANDLE_NUM_INDICES)
                 p = (MPIR_Op *) (void *) ((char *) (*MPIR_Op_mem.indirect)[MPIR_HANDLE_BLOCK(a)] +
                                           (size_t) MPIR_HANDLE_BLOCK_INDEX(a) * MPIR_Op_mem.size);
-            pthread_mutex_unlock(&op_mem_lock);
+            MPIR_Dropin_cs_exit(MPIR_DROPIN_CS_HANDLE);
             return p;
         }
     default:
@@ -138,7 +158,7 @@ MPIR_Op *MPIR_Op_get_ptr_fn(MPI_Op op)
 int MPIR_Op_create_impl(MPI_User_function * user_fn, int commute, MPI_Op * op)
 {
     MPIR_Op *op_ptr;
-    pthread_mutex_lock(&op_mem_lock);
+    MPIR_Dropin_cs_enter(MPIR_DROPIN_CS_HANDLE);     /* MPIR_Handle_obj_alloc */
     op_ptr = obj_alloc();
     if (op_ptr) {
         op_ptr->language = MPIR_LANG__C;
@@ -146,7 +166,7 @@ int MPIR_Op_create_impl(MPI_User_function * user_fn, int commute, MPI_Op * op)
         op_ptr->function.c_function = (void (*)(const void *, void *, const int *, const MPI_Datatype *)) user_fn;
         __atomic_store_n(&op_ptr->ref_count, 1, __ATOMIC_RELAXED);     /* MPIR_Object_set_ref */
     }
-    pthread_mutex_unlock(&op_mem_lock);
+    MPIR_Dropin_cs_exit(MPIR_DROPIN_CS_HANDLE);
     if (!op_ptr) {
         MPIR_Err_set_detail("Out of memory (MPI_Op)");      /* "**nomem %s" */
         return MPI_ERR_OTHER;
@@ -155,15 +175,16 @@ int MPIR_Op_create_impl(MPI_User_function * user_fn, int commute, MPI_Op * op)
     return MPI_SUCCESS;
 }
 
-/* MPIR_Op_free_impl (op_free.c:33-49): release one reference, free at zero */
+/* MPIR_Op_free_impl (op_free.c:33-49): release one reference
+ * (MPIR_Op_ptr_release_ref, atomic like MPICH's lock-free ref counts), and
+ * at zero MPIR_Handle_obj_free under the HANDLE section */
 void MPIR_Op_free_impl(MPI_Op * op)
 {
     MPIR_Op *op_ptr = MPIR_Op_get_ptr_fn(*op);
-    if (op_ptr) {
-        pthread_mutex_lock(&op_mem_lock);
-        if (__atomic_sub_fetch(&op_ptr->ref_count, 1, __ATOMIC_ACQ_REL) == 0)
-            obj_free(op_ptr);
-        pthread_mutex_unlock(&op_mem_lock);
+    if (op_ptr && __atomic_sub_fetch(&op_ptr->ref_count, 1, __ATOMIC_ACQ_REL) == 0) {
+        MPIR_Dropin_cs_enter(MPIR_DROPIN_CS_HANDLE);
+        obj_free(op_ptr);
+        MPIR_Dropin_cs_exit(MPIR_DROPIN_CS_HANDLE);
     }
     *op = MPI_OP_NULL;
 }

@@ -11,7 +11,8 @@
  * reset/read protocol and the builtin/user dispatch are the reference's.
  * Differences, all documented in DESIGN.md:
  *   - the library is always "initialized" (no MPI_Init in this drop-in);
- *   - error codes are the bare error classes (MPI_Error_class(c) == c);
+ *   - error codes are MPICH-format codes with an error stack (errutil.c; libmpi's
+ *     own MPIR_Err_* routines when compiled into it);
  *   - the error handler that MPI_Reduce_local reaches through
  *     MPIR_Err_return_comm(NULL, ...) is set by MPIX_Reduce_local_set_errhandler
  *     (default MPI_ERRORS_ARE_FATAL, as for COMM_WORLD in the reference);
@@ -253,7 +254,9 @@ int MPIR_Reduce_local(const void *inbuf, void *inoutbuf, int count, MPI_Datatype
 int MPIR_Reduce_local_checked(const void *inbuf, void *inoutbuf, int count, MPI_Datatype datatype, MPI_Op op)
 {
     static const char FCNAME[] = "PMPI_Reduce_local";
-    int mpi_errno = validate(inbuf, inoutbuf, count, datatype, op);
+    int mpi_errno;
+    MPIR_Dropin_cs_enter(MPIR_DROPIN_CS_GLOBAL);         /* reduce_local.c:162 */
+    mpi_errno = validate(inbuf, inoutbuf, count, datatype, op);
     if (mpi_errno == MPI_SUCCESS)
         mpi_errno = MPIR_Reduce_local(inbuf, inoutbuf, count, datatype, op);
     if (mpi_errno != MPI_SUCCESS) {
@@ -264,6 +267,7 @@ int MPIR_Reduce_local_checked(const void *inbuf, void *inoutbuf, int count, MPI_
                                          inoutbuf, count, datatype, op);
         mpi_errno = MPIR_Err_return_comm(NULL, FCNAME, mpi_errno);
     }
+    MPIR_Dropin_cs_exit(MPIR_DROPIN_CS_GLOBAL);          /* reduce_local.c:205 */
     return mpi_errno;
 }
 
@@ -279,8 +283,23 @@ int MPI_Reduce_local(const void *inbuf, void *inoutbuf, int count, MPI_Datatype 
 #endif
 
 /* ---- MPIX_Reduce_local_stream: enqueue on a HIP stream, no wait -------- */
+static int reduce_local_stream(const void *inbuf, void *inoutbuf, int count, MPI_Datatype datatype,
+                               MPI_Op op, void *hip_stream);
+
+/* the MPIX entry points validate user-op handles like MPI_Reduce_local does,
+ * so they hold the same GLOBAL section */
 int MPIX_Reduce_local_stream(const void *inbuf, void *inoutbuf, int count, MPI_Datatype datatype,
                              MPI_Op op, void *hip_stream)
+{
+    int rc;
+    MPIR_Dropin_cs_enter(MPIR_DROPIN_CS_GLOBAL);
+    rc = reduce_local_stream(inbuf, inoutbuf, count, datatype, op, hip_stream);
+    MPIR_Dropin_cs_exit(MPIR_DROPIN_CS_GLOBAL);
+    return rc;
+}
+
+static int reduce_local_stream(const void *inbuf, void *inoutbuf, int count, MPI_Datatype datatype,
+                               MPI_Op op, void *hip_stream)
 {
     int mpi_errno = validate(inbuf, inoutbuf, count, datatype, op);
     int opidx, elem, rc;
@@ -311,8 +330,21 @@ int MPIX_Reduce_local_stream(const void *inbuf, void *inoutbuf, int count, MPI_D
 }
 
 /* ---- MPIX_Reduce_local_multi: fused schedule steps (see the header) ---- */
+static int reduce_local_multi(const void *const *inbufs, int n, void *outbuf, int count,
+                              MPI_Datatype datatype, MPI_Op op, int order, void *hip_stream);
+
 int MPIX_Reduce_local_multi(const void *const *inbufs, int n, void *outbuf, int count,
                             MPI_Datatype datatype, MPI_Op op, int order, void *hip_stream)
+{
+    int rc;
+    MPIR_Dropin_cs_enter(MPIR_DROPIN_CS_GLOBAL);
+    rc = reduce_local_multi(inbufs, n, outbuf, count, datatype, op, order, hip_stream);
+    MPIR_Dropin_cs_exit(MPIR_DROPIN_CS_GLOBAL);
+    return rc;
+}
+
+static int reduce_local_multi(const void *const *inbufs, int n, void *outbuf, int count,
+                              MPI_Datatype datatype, MPI_Op op, int order, void *hip_stream)
 {
     static const char *fc = "MPIX_Reduce_local_multi";
     int mpi_errno, opidx, elem, rc, j;
@@ -372,10 +404,13 @@ int MPIX_Reduce_local_multi(const void *const *inbufs, int n, void *outbuf, int 
 /* ---- MPI_Op_create / MPI_Op_free / MPI_Op_commutative ------------------ */
 int PMPI_Op_create(MPI_User_function * user_fn, int commute, MPI_Op * op)
 {
-    int mpi_errno = MPIR_Op_create_impl(user_fn, commute, op);
+    int mpi_errno;
+    MPIR_Dropin_cs_enter(MPIR_DROPIN_CS_GLOBAL);         /* op_create.c:151 */
+    mpi_errno = MPIR_Op_create_impl(user_fn, commute, op);
     if (mpi_errno != MPI_SUCCESS)
-        return err_return("PMPI_Op_create", mpi_errno);
-    return MPI_SUCCESS;
+        mpi_errno = err_return("PMPI_Op_create", mpi_errno);
+    MPIR_Dropin_cs_exit(MPIR_DROPIN_CS_GLOBAL);
+    return mpi_errno;
 }
 
 int MPI_Op_create(MPI_User_function * user_fn, int commute, MPI_Op * op)
@@ -384,16 +419,19 @@ int MPI_Op_create(MPI_User_function * user_fn, int commute, MPI_Op * op)
 /* op_free.c:79-122: a predefined op is "**permop" */
 int PMPI_Op_free(MPI_Op * op)
 {
+    int mpi_errno = MPI_SUCCESS;
+    MPIR_Dropin_cs_enter(MPIR_DROPIN_CS_GLOBAL);         /* op_free.c:86 */
     if (HANDLE_GET_KIND(*op) == HANDLE_KIND_BUILTIN && HANDLE_GET_MPI_KIND(*op) == MPIR_OP_OBJ_KIND) {
         MPIR_Err_set_detail("Cannot free permanent MPI_Op");       /* "**permop" */
-        return err_return("PMPI_Op_free", MPI_ERR_OP);
-    }
-    if (!user_op_get(*op)) {
+        mpi_errno = err_return("PMPI_Op_free", MPI_ERR_OP);
+    } else if (!user_op_get(*op)) {
         MPIR_Err_set_detail("Invalid MPI_Op");
-        return err_return("PMPI_Op_free", MPI_ERR_OP);
+        mpi_errno = err_return("PMPI_Op_free", MPI_ERR_OP);
+    } else {
+        MPIR_Op_free_impl(op);
     }
-    MPIR_Op_free_impl(op);
-    return MPI_SUCCESS;
+    MPIR_Dropin_cs_exit(MPIR_DROPIN_CS_GLOBAL);          /* op_free.c:120 */
+    return mpi_errno;
 }
 
 int MPI_Op_free(MPI_Op * op) __attribute__ ((weak, alias("PMPI_Op_free")));
@@ -411,18 +449,21 @@ int MPIR_Op_is_commutative(MPI_Op op)
 /* op_commutative.c:101-140 */
 int PMPI_Op_commutative(MPI_Op op, int *commute)
 {
-    MPIR_Op *op_ptr;
-    if (HANDLE_GET_KIND(op) != HANDLE_KIND_BUILTIN) {
+    MPIR_Op *op_ptr = NULL;
+    int mpi_errno;
+    MPIR_Dropin_cs_enter(MPIR_DROPIN_CS_GLOBAL);         /* op_commutative.c:109 */
+    if (HANDLE_GET_KIND(op) != HANDLE_KIND_BUILTIN)
         op_ptr = user_op_get(op);
-        if (!op_ptr) {
-            MPIR_Err_set_detail("Invalid MPI_Op");
-            return err_return("PMPI_Op_commutative", MPI_ERR_OP);
-        }
-    } else if (HANDLE_GET_MPI_KIND(op) != MPIR_OP_OBJ_KIND || !(op_ptr = MPIR_Op_get_ptr_fn(op))) {
+    else if (HANDLE_GET_MPI_KIND(op) == MPIR_OP_OBJ_KIND)
+        op_ptr = MPIR_Op_get_ptr_fn(op);
+    if (!op_ptr) {
         MPIR_Err_set_detail("Invalid MPI_Op");
-        return err_return("PMPI_Op_commutative", MPI_ERR_OP);
+        mpi_errno = err_return("PMPI_Op_commutative", MPI_ERR_OP);
+    } else {
+        mpi_errno = MPIR_Op_commutative(op_ptr, commute);
     }
-    return MPIR_Op_commutative(op_ptr, commute);
+    MPIR_Dropin_cs_exit(MPIR_DROPIN_CS_GLOBAL);          /* op_commutative.c:136 */
+    return mpi_errno;
 }
 
 int MPI_Op_commutative(MPI_Op op, int *commute) __attribute__ ((weak, alias("PMPI_Op_commutative")));

@@ -11,22 +11,36 @@ import os
 import re
 import subprocess
 
+import pytest
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB = os.path.join(ROOT, "mpich-pip_amd", "lib")
 
 
-def dropin_sources():
+def _make_var(name):
     mk = open(os.path.join(ROOT, "mpich-pip_amd", "Makefile")).read()
-    m = re.search(r"^DROPIN_SRC\s*:=\s*(.+)$", mk, re.M)
+    m = re.search(r"^%s\s*:=\s*(.+)$" % name, mk, re.M)
     return [os.path.join(ROOT, "mpich-pip_amd", s) for s in m.group(1).split()]
 
 
-def test_dropin_into_hidden_visibility_libmpi(tmp_path):
+def dropin_sources():
+    return _make_var("DROPIN_SRC")
+
+
+@pytest.mark.parametrize("granularity", [1, 2, 3], ids=["GLOBAL", "POBJ", "VCI"])
+def test_dropin_into_hidden_visibility_libmpi(tmp_path, granularity):
+    """Option 1 at each of MPICH's thread granularities: DROPIN_SRC + DROPIN_GLUE
+    built with -DMPIR_DROPIN_IN_LIBMPI against (a stand-in of) MPICH's mpiimpl.h.
+    mock_app.c checks op_errno through an unchanged schedule and 8 threads of
+    MPI_Op_create / MPI_Op_free racing a progress engine's inline releases."""
     so = str(tmp_path / "libmockmpi.so")
     inc = ["-I" + os.path.join(ROOT, "include"), "-I" + os.path.join(ROOT, "mpich-pip_amd", "csrc", "host"),
+           "-I" + os.path.join(ROOT, "tests", "progs", "mock_mpich"),
            "-I/opt/rocm/include", "-D__HIP_PLATFORM_AMD__"]
-    subprocess.run(["gcc", "-shared", "-fPIC", "-O2", "-std=gnu99", "-fvisibility=hidden", "-Wall", *inc,
+    subprocess.run(["gcc", "-shared", "-fPIC", "-O2", "-std=gnu99", "-fvisibility=hidden", "-Wall",
+                    "-DMPIR_DROPIN_IN_LIBMPI", "-DMOCK_GRANULARITY=%d" % granularity, *inc,
                     os.path.join(ROOT, "tests", "progs", "mock_libmpi.c"), *dropin_sources(),
+                    *_make_var("DROPIN_GLUE"),
                     "-L" + LIB, "-lmpir_hip", "-Wl,-rpath," + LIB, "-lpthread", "-o", so], check=True)
     dyn = subprocess.run(["nm", "-D", "--defined-only", so], capture_output=True, text=True, check=True).stdout
     exported = {ln.split()[-1] for ln in dyn.splitlines() if ln.strip()}
@@ -34,14 +48,16 @@ def test_dropin_into_hidden_visibility_libmpi(tmp_path):
                    "MPIX_Reduce_local_stream", "mock_sched_reduce"):
         assert public in exported, public
     for internal in ("MPIR_Reduce_local", "MPIR_Op_table", "MPIR_Op_direct", "MPIR_Op_mem", "MPIR_SUM",
-                     "MPIR_Err_create_code", "MPIR_Err_return_comm"):
+                     "MPIR_Err_create_code", "MPIR_Err_return_comm", "MPIR_Op_errno_ptr", "MPIR_Dropin_cs_enter"):
         assert internal not in exported, internal
     app = str(tmp_path / "mock_app")
-    subprocess.run(["gcc", "-std=c99", "-Wall", "-Werror", "-I" + os.path.join(ROOT, "include"),
+    subprocess.run(["gcc", "-std=gnu99", "-Wall", "-Werror", "-I" + os.path.join(ROOT, "include"),
                     os.path.join(ROOT, "tests", "progs", "mock_app.c"), so, "-Wl,-rpath," + str(tmp_path),
-                    "-o", app], check=True)
-    r = subprocess.run([app], capture_output=True, text=True, timeout=120)
-    assert r.returncode == 0, r.stderr
+                    "-ldl", "-lpthread", "-o", app], check=True)
+    # no device visible: the host combine runs without one (CPU-only rank)
+    env = dict(os.environ, HIP_VISIBLE_DEVICES="-1")
+    r = subprocess.run([app], capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stdout + r.stderr
     assert "mock libmpi ok" in r.stdout
 
 

@@ -683,6 +683,41 @@ def test_host_path_matrix_vs_oracle(mpi, orc, cuda, op, t):
         run_pair_host(mpi, orc, op, t, n, seed, off)
 
 
+@pytest.mark.parametrize("path", ["host_combine", "mixed_slot"])
+def test_pinned_host_operand_ordered_after_null_stream(mpi, orc, cuda, path):
+    """A pinned host operand filled by an async D2H copy on the legacy null
+    stream, queued behind slow device work, is read only after that copy lands:
+    the host combine (both operands host) and the mixed path's slot copy (host
+    inbuf, device inoutbuf) first synchronise with the null stream, as the
+    device path does (hip_reduce.hip order_after_null_stream)."""
+    import torch
+    n = (256 << 10) if path == "mixed_slot" else (8 << 20)          # mixed: <= 1 MiB per operand
+    rng = np.random.default_rng(77)
+    a = rng.uniform(-1, 1, n).astype(np.float32)                   # inout
+    b = rng.uniform(-1, 1, n).astype(np.float32)                   # in (arrives by D2H)
+    want = a.copy()
+    assert orc.reduce_local(b.copy(), want, n, mpi.MPI_FLOAT, mpi.MPI_SUM) == 0
+    for rep in range(3):
+        db = torch.from_numpy(b).cuda()
+        big = torch.ones(64 << 20, device="cuda")
+        torch.cuda.synchronize()
+        hb = torch.full((n,), float("nan"), dtype=torch.float32).pin_memory()
+        if path == "host_combine":
+            ha = torch.from_numpy(a.copy()).pin_memory()
+            io = ha.data_ptr()
+        else:
+            da = torch.from_numpy(a.copy()).cuda()
+            io = da.data_ptr()
+        torch.cuda.synchronize()
+        for _ in range(20):                  # ~ms of work on the null stream ahead of the copy
+            big.mul_(1.0000001)
+        hb.copy_(db, non_blocking=True)      # D2H into pinned memory, null stream, returns at once
+        rc = mpi.reduce_local(hb.data_ptr(), io, n, mpi.MPI_FLOAT, mpi.MPI_SUM)
+        assert rc == 0, mpi.error_string(rc)
+        got = ha.numpy() if path == "host_combine" else da.cpu().numpy()
+        assert np.array_equal(got.view(np.uint32), want.view(np.uint32)), (path, rep)
+
+
 def test_host_path_crossover(mpi, orc, cuda):
     """Either side of a host limit set with MPIR_Hip_set_host_max_bytes (host
     combine below, GPU staging above; the default is no limit), and the host

@@ -2,8 +2,11 @@
 shared-memory world, MPI_Init/Comm_size/rank/Bcast/Barrier/Finalize, and
 MPI_Reduce's binomial schedule driven with a user-defined (host) op whose
 result fingerprints the exact combine order (reduce_intra_binomial.c:100-160).
-Builtin-op reductions need the HIP path: on a machine without a GPU they must
-fail loudly (no CPU fallback) -- checked here; their values are checked in
+Builtin-op reductions on host buffers run the library's host combine (the
+kernels' functors compiled for the host -- product code, not the oracle), which
+needs no device, as the reference's loop (opsum.c:21) runs anywhere: cpi's
+golden line and MPI_Reduce's schedules are checked here on a CPU-only rank
+(HIP_VISIBLE_DEVICES=-1) against the oracle, and again with a GPU visible in
 test_pip_runtime_gpu.py.
 """
 import os
@@ -31,9 +34,12 @@ def prog(tmp_path_factory, mpi):
     return build_prog(tmp_path_factory)
 
 
-def run(n, *cmd, timeout=120):
+def run(n, *cmd, timeout=120, env=None):
     return subprocess.run([MPIEXEC, "-n", str(n), "--timeout", str(timeout - 10), *cmd],
-                          capture_output=True, text=True, timeout=timeout)
+                          capture_output=True, text=True, timeout=timeout, env=env)
+
+
+NO_GPU = dict(os.environ, HIP_VISIBLE_DEVICES="-1")
 
 
 def val(rank, i):
@@ -108,14 +114,22 @@ def test_mismatched_counts_error_not_hang(prog, n):
         assert red == (14 if rank == 0 else 0), rank
 
 
-def test_builtin_reduce_without_gpu_fails_loudly(prog, mpi):
-    if mpi.load().MPIR_Hip_device_count() > 0:
-        pytest.skip("a GPU is visible: covered by test_pip_runtime_gpu.py")
-    cpi = os.path.join(ROOT, "examples", "cpi")
-    r = run(2, cpi)
-    assert r.returncode == 1
-    assert "Fatal error in MPI_Reduce" in r.stderr and "no HIP device available" in r.stderr
-    assert "pi is approximately" not in r.stdout
+def test_cpi_np2_golden_cpu_only_rank():
+    """cpi on ranks that see no GPU: every MPI_Reduce combine step is a host
+    combine; the reference's golden line."""
+    r = run(2, os.path.join(ROOT, "examples", "cpi"), env=NO_GPU)
+    assert r.returncode == 0, r.stderr
+    assert "pi is approximately 3.1415926544231318, Error is 0.0000000008333387" in r.stdout
+
+
+@pytest.mark.parametrize("p", [2, 3, 5, 8])
+def test_builtin_reduce_schedules_cpu_only_rank(prog, orc, mpi, p):
+    """Builtin MPI_SUM MPI_Reduce of 1 and 4099 doubles on every root with no
+    device visible: bit-identical to the oracle's step-by-step schedules."""
+    from test_pip_runtime_gpu import check_builtin_reduce_rows
+    r = run(p, prog, "gpu", timeout=300, env=NO_GPU)
+    assert r.returncode == 0, r.stderr
+    check_builtin_reduce_rows(parse(r.stdout), p, mpi)
 
 
 def test_cpi_singleton_needs_no_reduction():
