@@ -15,13 +15,21 @@ torch.cuda.synchronize() on both sides, after W untimed warm-up steps.
     value = 3 * 256 MiB * K * N / max_rank_seconds / 2^30   (GiB/s, algorithmic bytes:
             read inbuf, read inoutbuf, write inoutbuf -- SURVEY.md §8d)
 
-Runtime: HSA_ALLOCATE_QUEUE_DEV_MEM=1 (ROCm's knob for AQL rings in device
-memory, read once when the HSA runtime starts) unless the environment sets
-it: the CP then fetches each dispatch packet from VRAM instead of over PCIe,
-1.4 us off every synchronous call (profiles/r02/sync_ab_ring.log).
-The library's own launcher (bin/mpiexec) sets the same default for its ranks.
+Runtime: nothing is tuned by the bench.  The library (libmpir_hip.so) defaults
+HSA_ALLOCATE_QUEUE_DEV_MEM to 1 when it is loaded -- before the HSA runtime
+starts -- unless the environment sets it: AQL rings in VRAM, the CP fetches each
+dispatch packet locally, 1.4 us off every synchronous call.  The
+bench therefore loads the library before its first GPU call, as a program linked
+against libmpi does before main().  `value` is that default; `sync_variants`
+shows what the headline loop gives without it and without kernarg-cache hits.
 
 Extra fields (rank 0):
+  value_conditions  what `value` was measured under (the headline).
+  sync_variants the headline loop again with fresh kernel arguments on every
+                call (each misses the kernarg cache: BAR write + HDP flush), and
+                -- in a child process started before this one touches the GPU --
+                with HSA_ALLOCATE_QUEUE_DEV_MEM=0 (ROCm's own ring placement),
+                with cached and with fresh arguments (N = 1).
   roofline      dominant kernel: mpir_tile_SUM_MPIR_HIP_F32, which the synchronous
                 call dispatches on the library's own AQL queue (direct_dispatch.hip);
                 its duration is the CP's dispatch start / end timestamps
@@ -53,9 +61,6 @@ import sys
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
-# before torch (or anything) starts the HSA runtime; see the docstring
-RING_DEFAULTED = "HSA_ALLOCATE_QUEUE_DEV_MEM" not in os.environ
-os.environ.setdefault("HSA_ALLOCATE_QUEUE_DEV_MEM", "1")
 sys.path.insert(0, os.path.join(ROOT, "mpich-pip_amd"))
 sys.path.insert(0, ROOT)
 
@@ -64,6 +69,8 @@ GIB = 1 << 30
 HBM_PEAK_BPS = 8.0e12          # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 METRIC = "GiB/s device-resident MPI_Reduce_local (fp32 SUM, 256 MiB) at 1/2/4/8 GPUs"
 NPAIRS = 4                     # operand pairs rotated through (>= 3)
+FRESH_OFFSETS = 256            # fresh-argument loop: 256 B steps x NPAIRS = 1024 distinct argument sets
+SLACK = FRESH_OFFSETS * 256    # bytes past each operand the fresh-argument offsets reach into
 
 
 def parse():
@@ -83,6 +90,8 @@ def parse():
     ap.add_argument("--cpu-standin", action="store_true",
                     help="TEST ONLY: gloo + a numpy step instead of the GPU call, to exercise the rank "
                          "launch and the max-over-ranks timing on a machine without GPUs")
+    ap.add_argument("--no-variants", action="store_true", help="skip sync_variants")
+    ap.add_argument("--variant-child", action="store_true", help=argparse.SUPPRESS)
     return ap.parse_args()
 
 
@@ -165,10 +174,6 @@ def run_collectives_child(rank: int, world: int, local: int, barrier, timeout: f
     barrier()
     env = dict(os.environ, RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(local),
                COLL_STORE_PORT=str(int(os.environ.get("MASTER_PORT", "29500")) + 101))
-    if RING_DEFAULTED:
-        # configs 4-5 are RCCL-bound: they run on ROCm's default queue placement
-        # (the VRAM-ring default is measured on the synchronous path only)
-        env.pop("HSA_ALLOCATE_QUEUE_DEV_MEM", None)
     p = subprocess.Popen([sys.executable, os.path.join(ROOT, "bench_coll.py")], env=env,
                          stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, start_new_session=True)
     try:
@@ -183,6 +188,84 @@ def run_collectives_child(rank: int, world: int, local: int, barrier, timeout: f
     if rank == 0:
         return json.loads(lines[-1]) if lines else {"error": "no output"}
     return {}
+
+
+def sync_loops(m, lib, reduce_local, ptrs, count, k: int, w: int, sync, barrier, max_over_ranks):
+    """The headline loop (NPAIRS pairs rotated: every call after the first
+    NPAIRS repeats its kernel arguments, which the direct dispatch's kernarg
+    cache then holds) and the same loop with fresh arguments on every call: the
+    pairs shifted by multiples of 256 B (same count, same alignment, same
+    kernel), 1024 distinct argument sets, so every call writes its arguments
+    into a VRAM slot and flushes the HDP first.  Returns seconds of each and
+    the kernarg writes per timed fresh call."""
+    dt_f32, op_sum = m.MPI_FLOAT, m.MPI_SUM
+    call_args = [(pin, pio, count, dt_f32, op_sum) for pin, pio in ptrs]
+    fresh_args = [(pin + o, pio + o, count, dt_f32, op_sum) for o in range(0, SLACK, 256) for pin, pio in ptrs]
+
+    def step(i):
+        rc = reduce_local(*call_args[i % NPAIRS])
+        if rc:
+            raise RuntimeError(m.error_string(rc))
+
+    def fstep(i):
+        rc = reduce_local(*fresh_args[i % len(fresh_args)])
+        if rc:
+            raise RuntimeError(m.error_string(rc))
+    dt = time_steps(step, k, w, sync, barrier, max_over_ranks)
+    kw0 = lib.MPIR_Hip_direct_kernarg_writes()
+    dtf = time_steps(fstep, k, w, sync, barrier, max_over_ranks)
+    writes = (lib.MPIR_Hip_direct_kernarg_writes() - kw0) / (k + w)
+    return dt, dtf, writes, step
+
+
+def process_env(name: str) -> str:
+    """The variable as the C runtime holds it (the library may have set it at
+    load; os.environ is Python's snapshot from start-up)."""
+    import ctypes
+    libc = ctypes.CDLL(None)
+    libc.getenv.restype = ctypes.c_char_p
+    v = libc.getenv(name.encode())
+    return v.decode() if v is not None else ""
+
+
+def variant_child(args) -> None:
+    """--variant-child: the headline loop and its fresh-argument twin in this
+    process's environment (the parent sets HSA_ALLOCATE_QUEUE_DEV_MEM=0);
+    one JSON line."""
+    import torch
+    import mpich_pip_amd as m
+    lib = m.load()
+    lib.MPIX_Reduce_local_set_errhandler(m.MPI_ERRORS_RETURN)
+    reduce_local = m.fast_reduce_local()
+    torch.cuda.set_device(0)
+    count = args.mib * MIB // 4
+    g = torch.Generator(device="cuda").manual_seed(0x5EED)
+    pairs = [((torch.rand(count + SLACK // 4, device="cuda", generator=g) * 2 - 1),
+              (torch.rand(count + SLACK // 4, device="cuda", generator=g) * 2 - 1)) for _ in range(NPAIRS)]
+    torch.cuda.synchronize()
+    ptrs = [(a.data_ptr(), b.data_ptr()) for a, b in pairs]
+    dt, dtf, writes, _ = sync_loops(m, lib, reduce_local, ptrs, count, args.steps, args.warmup,
+                                    torch.cuda.synchronize, lambda: None, lambda x: x)
+    print(json.dumps({"dt": dt, "dt_fresh": dtf, "kernarg_writes_per_fresh_call": writes,
+                      "HSA_ALLOCATE_QUEUE_DEV_MEM": process_env("HSA_ALLOCATE_QUEUE_DEV_MEM"),
+                      "direct_state": lib.MPIR_Hip_direct_state(0)}), flush=True)
+
+
+def run_variant_child(args) -> dict:
+    """Start --variant-child with ROCm's own AQL ring placement
+    (HSA_ALLOCATE_QUEUE_DEV_MEM=0); called before this process touches a GPU."""
+    import subprocess
+    env = dict(os.environ, HSA_ALLOCATE_QUEUE_DEV_MEM="0")
+    cmd = [sys.executable, os.path.abspath(__file__), "--variant-child", "--steps", str(args.steps),
+           "--warmup", str(args.warmup), "--mib", str(args.mib)]
+    try:
+        r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=240)
+    except subprocess.TimeoutExpired:
+        return {"error": "timeout"}
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    if r.returncode != 0 or not lines:
+        return {"error": f"exit {r.returncode}", "stderr_tail": r.stderr.strip().splitlines()[-3:]}
+    return json.loads(lines[-1])
 
 
 def event_launch_us(launch, k: int, w: int, stream, stat: str = "mean") -> float:
@@ -423,13 +506,22 @@ def main():
         sys.exit(rc)
     if args.cpu_standin:
         return cpu_standin(args)
-    import torch
-    import torch.distributed as dist
-    import mpich_pip_amd as m
-
+    if args.variant_child:
+        return variant_child(args)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # ROCm's own ring placement, in a child, before this process starts the GPU
+    ring_variant = None
+    if world == 1 and not args.no_extras and not args.no_variants:
+        ring_variant = run_variant_child(args)
+    import torch
+    import torch.distributed as dist
+    import mpich_pip_amd as m
+    # the library first, as a program linked against libmpi loads it before main():
+    # it defaults the AQL rings into VRAM before the HSA runtime starts
+    lib = m.load()
+    lib.MPIX_Reduce_local_set_errhandler(m.MPI_ERRORS_RETURN)
     if world != args.gpus:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world} (launched by an external launcher); "
               f"measuring WORLD_SIZE ranks", file=sys.stderr)
@@ -479,8 +571,6 @@ def main():
         return float(t.item())
 
     sync = torch.cuda.synchronize
-    lib = m.load()
-    lib.MPIX_Reduce_local_set_errhandler(m.MPI_ERRORS_RETURN)
 
     nbytes = args.mib * MIB
     count = nbytes // 4
@@ -488,8 +578,9 @@ def main():
     g = torch.Generator(device="cuda").manual_seed(0x5EED + rank)
     # NPAIRS resident pairs, rotated, so no step finds its operands in the
     # 256 MB Infinity Cache (>= 3 pairs)
-    pairs = [((torch.rand(count, device="cuda", generator=g) * 2 - 1),
-              (torch.rand(count, device="cuda", generator=g) * 2 - 1)) for _ in range(NPAIRS)]
+    # (SLACK bytes past each operand: the fresh-argument loop's offsets)
+    pairs = [((torch.rand(count + SLACK // 4, device="cuda", generator=g) * 2 - 1),
+              (torch.rand(count + SLACK // 4, device="cuda", generator=g) * 2 - 1)) for _ in range(NPAIRS)]
     ptrs = [(a.data_ptr(), b.data_ptr()) for a, b in pairs]
     sync()
 
@@ -499,17 +590,14 @@ def main():
         reduce_local, binding = m.fast_reduce_local(), "compiled CPython binding (csrc/py/fastcall.c)"
     except ImportError:     # extension not built: the same C entry point through ctypes
         reduce_local, binding = lib.MPI_Reduce_local, "ctypes"
-    dt_f32, op_sum = m.MPI_FLOAT, m.MPI_SUM
-
-    call_args = [(pin, pio, count, dt_f32, op_sum) for pin, pio in ptrs]
-
-    def step(i):
-        rc = reduce_local(*call_args[i % NPAIRS])
-        if rc:
-            raise RuntimeError(m.error_string(rc))
-
-    dt = time_steps(step, args.steps, args.warmup, sync, barrier, max_over_ranks)
+    dt, dt_fresh, fresh_writes, step = sync_loops(m, lib, reduce_local, ptrs, count, args.steps, args.warmup,
+                                                  sync, barrier, max_over_ranks)
     value = alg_bytes * args.steps * world / dt / GIB
+
+    def rate(seconds):
+        v = alg_bytes * args.steps * world / seconds / GIB
+        return {"value": round(v, 1), "frac_of_hbm_peak": round(v / world * GIB / HBM_PEAK_BPS, 4),
+                "ms_per_step": round(seconds / args.steps * 1e3, 4)}
 
     out = {
         "metric": METRIC,
@@ -531,15 +619,36 @@ def main():
             "algorithmic_bytes_per_call": alg_bytes,
             "api": "MPI_Reduce_local (C ABI, synchronous; called through the " + binding + ")",
             "parallelism": "replica-per-gpu (no data-path collective)",
-            "runtime": {"HSA_ALLOCATE_QUEUE_DEV_MEM": os.environ.get("HSA_ALLOCATE_QUEUE_DEV_MEM", "")},
+            "runtime": {"HSA_ALLOCATE_QUEUE_DEV_MEM": process_env("HSA_ALLOCATE_QUEUE_DEV_MEM"),
+                        "HSA_ALLOCATE_QUEUE_DEV_MEM_in_job_environment": os.environ.get("HSA_ALLOCATE_QUEUE_DEV_MEM")},
             "process_group": pg_backend,
         },
+        "value_conditions": {
+            "headline": "value",
+            "environment": "as launched: the bench sets no runtime variable; HSA_ALLOCATE_QUEUE_DEV_MEM is the "
+                           "library's load-time default (1) unless the job sets it (config.runtime)",
+            "kernel_arguments": "%d rotating pairs: every call after the first %d repeats its arguments (kernarg "
+                                "cache hit); sync_variants.fresh_args misses on every call" % (NPAIRS, NPAIRS)},
         # the synchronous call per GPU (launch + completion included) against the HBM peak
         "per_gpu": {"GiBps": round(value / world, 1),
                     "frac_of_hbm_peak": round(value / world * GIB / HBM_PEAK_BPS, 4),
                     # the buffer rate count * sizeof(T) / t, for readability
                     "buffer_GiBps": round(value / world / 3, 1)},
     }
+
+    variants = {"fresh_args": dict(rate(dt_fresh), kernarg_writes_per_call=round(fresh_writes, 3),
+                                   note="same loop, every call's arguments new (pairs shifted by multiples of "
+                                        "256 B, 1024 distinct sets): kernarg BAR write + HDP flush per call")}
+    if ring_variant is not None:
+        if "dt" in ring_variant:
+            variants["rocm_ring_placement"] = {
+                "env": "HSA_ALLOCATE_QUEUE_DEV_MEM=0 (child process)",
+                "cached_args": rate(ring_variant["dt"]), "fresh_args": rate(ring_variant["dt_fresh"]),
+                "HSA_ALLOCATE_QUEUE_DEV_MEM_seen": ring_variant.get("HSA_ALLOCATE_QUEUE_DEV_MEM"),
+                "direct_state": ring_variant.get("direct_state")}
+        else:
+            variants["rocm_ring_placement"] = ring_variant
+    out["sync_variants"] = variants
 
     if share:
         out["data"] = "REHEARSAL (BENCH_TEST_SHARE_GPU): %d ranks on %d GPU(s), not a measurement" % (

@@ -133,6 +133,9 @@ int MPIR_Hip_direct_state(int dev);
  * completion seen by the host. */
 void MPIR_Hip_direct_last_split(uint64_t out[4]);
 uint64_t MPIR_Hip_direct_busy_skips(void);
+/* Direct calls whose kernel arguments missed the kernarg cache (written into a
+ * VRAM slot and made visible with an HDP flush before the doorbell). */
+uint64_t MPIR_Hip_direct_kernarg_writes(void);
 int MPIR_Hip_thread_contexts(void);
 
 #ifdef __cplusplus

@@ -10,7 +10,8 @@
 // waits on the kernel packet's completion signal instead: 7.4-7.5 us, and the
 // 256 MiB fp32 SUM call 126.2-126.4 us against 127.6-127.8 (same box, same
 // kernel); with the kernarg cache below and the AQL rings in VRAM
-// (HSA_ALLOCATE_QUEUE_DEV_MEM=1) the gap is 5.2-5.5 us, 4.3 us of it the CP
+// (HSA_ALLOCATE_QUEUE_DEV_MEM=1, the library's default: default_rings_in_vram)
+// the gap is 5.2-5.5 us, 4.3 us of it the CP
 // noticing the doorbell (profiles/r02/sync_split_timeline.log, cp_latency.log).  An earlier attempt (round 1) lost because its kernargs sat in host
 // memory (every workgroup read them over PCIe); here they are written through
 // the BAR into VRAM and made visible with an HDP flush (the register ROCr
@@ -47,14 +48,11 @@
 #include <stdlib.h>
 #include <string.h>
 #include <pthread.h>
-#include <sched.h>
-#include <sys/prctl.h>
 #include <time.h>
 
 #include <atomic>
 #include <mutex>
 #include <string>
-#include <thread>
 #include <vector>
 
 #include "mpir_hip_reduce.h"
@@ -107,24 +105,12 @@ struct DevState {
     uint64_t kobj[kPlanKinds][MPIR_HIP_NOPS][MPIR_HIP_NELEMS] = {};   // by plan kind (kPlanPrefix)
     std::mutex publish;
     std::atomic<int> queue_error{0};
-    // keep-alive (keepalive_us()): its queue and no-op kernargs; on a line of
-    // their own, the monotonic time of the last call's end or keep-alive packet
-    // and whether a call is in flight (a busy CP is not idle: no keep-alive
-    // then).  Plain stores on the call path, no read-modify-write.
-    hsa_queue_t *kqueue = nullptr;              // created when the keep-alive is first armed
-    std::once_flag konce;
-    std::atomic<bool> kready{false};
-    char *kargs_noop = nullptr;
-    alignas(64) std::atomic<uint64_t> last_packet_ns{0};
-    std::atomic<uint64_t> last_call_ns{0};      // the keep-alive runs for a window after this
-    std::atomic<int> call_busy{0};
-    std::atomic<int> armed{0};                  // the caller has been seen to leave gaps
-    char pad_[64 - 2 * sizeof(std::atomic<uint64_t>) - 2 * sizeof(std::atomic<int>)];
 };
 
 DevState g_dev[kMaxDirectDev];
 std::atomic<uint64_t> g_direct_calls{0};
 std::atomic<uint64_t> g_busy_skips{0};      // calls that first synchronised with a busy null stream
+std::atomic<uint64_t> g_kernarg_writes{0};  // kernarg-cache misses (BAR write + HDP flush)
 // MPIX_Reduce_local_profile: the CP's start / end timestamps of each direct
 // dispatch (hsa_amd_profiling_get_dispatch_time, what rocprofv3 reads), so a
 // benchmark can time the kernel the synchronous call really runs
@@ -141,92 +127,6 @@ static inline uint64_t sys_ts() {
 }
 uint64_t g_ts_freq = 0;
 
-// MPIR_CVAR_REDUCE_LOCAL_WAIT_MWAITX=1 (A/B, AMD hosts with MONITORX): wait for
-// the completion signal's value line with MONITORX / MWAITX instead of a
-// pause loop (tools/mwaitx_ab.sh)
-bool use_mwaitx() {
-    static const bool v = [] {
-        const char *e = getenv("MPIR_CVAR_REDUCE_LOCAL_WAIT_MWAITX");
-        if (!e || atoi(e) == 0) return false;
-        unsigned a, b, c, dd;
-        __asm__ volatile("cpuid" : "=a"(a), "=b"(b), "=c"(c), "=d"(dd) : "a"(0x80000001u), "c"(0));
-        return ((c >> 29) & 1u) != 0;   // CPUID Fn8000_0001 ECX[29] = MONITORX
-    }();
-    return v;
-}
-
-__attribute__((target("mwaitx"))) void wait_signal_mwaitx(hsa_signal_t sig) {
-#if !defined(__HIP_DEVICE_COMPILE__)     // host code; the device pass never emits it
-    volatile int64_t *v = &reinterpret_cast<amd_signal_t *>(sig.handle)->value;
-    while (__atomic_load_n(v, __ATOMIC_ACQUIRE) != 0) {
-        __builtin_ia32_monitorx((void *)v, 0, 0);
-        if (__atomic_load_n(v, __ATOMIC_ACQUIRE) == 0) break;
-        __builtin_ia32_mwaitx(0x2, 0, 20000);   // ECX bit 1: EBX timer, at most ~20000 TSC ticks
-    }
-#else
-    (void)sig;
-#endif
-}
-
-uint64_t mono_ns() {
-    timespec t;
-    clock_gettime(CLOCK_MONOTONIC, &t);
-    return (uint64_t)t.tv_sec * 1000000000ull + (uint64_t)t.tv_nsec;
-}
-
-// Keep-alive: after 50-100 us without a packet the command processor drops
-// into a deeper idle state and the next doorbell takes ~10 us instead of ~5 to
-// start the kernel (tools/idle_gap_probe.py: a 4 MiB call 9.6 us after a 50 us
-// host gap, 14.9-15.5 us after 100 us-5 ms), which every combine step of a
-// schedule that waits on the network would pay.  A kernel in flight on another
-// queue does not prevent it (tools/idle_sleep_probe.py): it is the CP's
-// doorbell handling that sleeps.  MPIR_CVAR_REDUCE_LOCAL_KEEPALIVE_US = P
-// (opt-in, e.g. 40; default 0 = off -- with it on, bench.py's back-to-back loop
-// measured 0.763-0.786 against 0.79-0.80: profiles/r02/keepalive_default_bench.log): a call that arrives more than P + 10 us after the
-// previous one ends arms the keep-alive, one that arrives within P us disarms
-// it; while armed and within MPIR_CVAR_REDUCE_LOCAL_KEEPALIVE_MS (default 20)
-// of the last call, a library thread puts an empty barrier-AND packet on the
-// calls' own queue whenever no packet has gone for P us and no call is in
-// flight.  Sparse callers then take ~10 us after any gap instead of ~15, with
-// no slow outliers and no cost to back-to-back loops
-// (tools/keepalive_same_ab.sh, profiles/r02/keepalive_same_ab.log).  On a queue
-// of its own (_QUEUE=own) the packets made the hardware scheduler map one more
-// active queue: calls that met them took ~18 us longer (tools/ka_probe.py,
-// profiles/r02/ka_probe.log, keepalive_headline_ab.log, lazy_queues_ab.log).
-// _KIND=kernel (one workgroup of the SUM tile kernel with nothing to do) and
-// _QUEUE=same (the calls' queue) are the A/B's other variants, no better.
-// Idle for longer than the window, the thread naps 1 ms at a time.
-int keepalive_us() {
-    static const int v = [] {
-        const char *e = getenv("MPIR_CVAR_REDUCE_LOCAL_KEEPALIVE_US");
-        const int us = e ? atoi(e) : 0;
-        return us > 0 && us <= 100000 ? us : 0;
-    }();
-    return v;
-}
-int keepalive_kernel() {
-    static const int v = [] {
-        const char *e = getenv("MPIR_CVAR_REDUCE_LOCAL_KEEPALIVE_KIND");
-        return (e && !strcmp(e, "kernel")) ? 1 : 0;
-    }();
-    return v;
-}
-int keepalive_own_queue() {
-    static const int v = [] {
-        const char *e = getenv("MPIR_CVAR_REDUCE_LOCAL_KEEPALIVE_QUEUE");
-        return (e && !strcmp(e, "own")) ? 1 : 0;
-    }();
-    return v;
-}
-uint64_t keepalive_active_ns() {
-    static const uint64_t v = [] {
-        const char *e = getenv("MPIR_CVAR_REDUCE_LOCAL_KEEPALIVE_MS");
-        const long ms = e ? atol(e) : 20;
-        return (uint64_t)(ms > 0 && ms <= 60000 ? ms : 20) * 1000000ull;
-    }();
-    return v;
-}
-
 int mode() {
     static const int m = [] {
         const char *e = getenv("MPIR_CVAR_REDUCE_LOCAL_DISPATCH");
@@ -235,55 +135,37 @@ int mode() {
     return m;
 }
 
-// Dispatch timestamps cost the synchronous call ~0.4 us at 256 MiB and ~0.9 us
-// at 64 MiB (the CP writes start / end times per packet; alternated processes,
-// tools/ts_ab.sh, profiles/r02/ts_ab.log), and switching them on for a live
-// queue does not take effect (tools/ts_enable_probe.py).  So the calls' queue
-// runs without them and a second queue, created with them on, takes the calls
-// made while MPIR_Hip_direct_profile is on (the bench's roofline readout: the
-// same kernel object, plan and arguments).
-// MPIR_CVAR_REDUCE_LOCAL_DIRECT_TIMESTAMPS=1 turns them on for the calls' queue
-// too (the round-2 behaviour, for A/Bs).
-int timestamps() {
-    static const int t = [] {
-        const char *e = getenv("MPIR_CVAR_REDUCE_LOCAL_DIRECT_TIMESTAMPS");
-        return e ? (atoi(e) != 0) : 0;
-    }();
-    return t;
-}
+// The calls' queue records no dispatch timestamps: with them the CP's
+// per-packet timestamp writes cost the synchronous call ~0.4 us at 256 MiB and
+// ~0.9 us at 64 MiB (alternated processes, tools/ts_ab.sh, profiles/r02/ts_ab.log),
+// and switching them on for a live queue does not take effect
+// (tools/ts_enable_probe.py).  A second queue, created with them on, takes the
+// calls made while MPIR_Hip_direct_profile is on (the bench's roofline readout:
+// the same kernel object, plan and arguments).
+//
+// Packet fences: agent-scope acquire (what HIP uses between kernels; a
+// system-scope acquire costs ~7 us of kernel body, aql_sig_nt_sys) and
+// system-scope release, so the result is visible to every agent -- SDMA copies
+// and the host included -- when the signal fires.  Other scopes measured within
+// 0.2 us (tools/scope_ab.sh, profiles/r02/scope_ab.log); none at release would
+// leave results in one XCD's L2 and is not offered.
+constexpr int kAcquireScope = HSA_FENCE_SCOPE_AGENT;
+constexpr int kReleaseScope = HSA_FENCE_SCOPE_SYSTEM;
 
-// packet fence scopes (experiments: MPIR_CVAR_REDUCE_LOCAL_DIRECT_ACQUIRE /
-// _RELEASE = none | agent | system); defaults agent acquire, system release
-static int scope_env(const char *name, int dflt) {
-    const char *e = getenv(name);
-    if (!e) return dflt;
-    if (!strcmp(e, "none")) return HSA_FENCE_SCOPE_NONE;
-    if (!strcmp(e, "agent")) return HSA_FENCE_SCOPE_AGENT;
-    if (!strcmp(e, "system")) return HSA_FENCE_SCOPE_SYSTEM;
-    return dflt;
-}
-int acquire_scope() {
-    static const int v = scope_env("MPIR_CVAR_REDUCE_LOCAL_DIRECT_ACQUIRE", HSA_FENCE_SCOPE_AGENT);
-    return v;
-}
-int release_scope() {
-    static const int v = scope_env("MPIR_CVAR_REDUCE_LOCAL_DIRECT_RELEASE", HSA_FENCE_SCOPE_SYSTEM);
-    return v;
-}
-
-// MPIR_CVAR_REDUCE_LOCAL_DIRECT_SIGNAL: "memory" (default, 0) or "interrupt" (1)
-int signal_kind() {
-    static const int k = [] {
-        const char *e = getenv("MPIR_CVAR_REDUCE_LOCAL_DIRECT_SIGNAL");
-        return (e && !strcmp(e, "interrupt")) ? 1 : 0;
-    }();
-    return k;
-}
-
+// HIP's device -> its HSA agent.  The device's UUID (hipDeviceProp_t::uuid,
+// the 16 characters after "GPU-" of HSA_AMD_AGENT_INFO_UUID) identifies it when
+// it matches exactly one agent; otherwise its PCI domain and bus / device
+// numbers must match exactly one agent.  Compute-partitioned GPUs expose
+// several agents with one bus / device number (the function bits, which HIP's
+// properties do not carry, tell them apart): with no unique match the direct
+// path is refused (MPIR_Hip_direct_state -3) rather than guessed.
 struct Find {
     uint32_t bdf, domain;
-    hsa_agent_t gpu{}, cpu{};
-    bool have_gpu = false, have_cpu = false;
+    char uuid[16];
+    bool have_uuid = false;
+    hsa_agent_t bdf_gpu{}, uuid_gpu{}, cpu{};
+    int bdf_matches = 0, uuid_matches = 0;
+    bool have_cpu = false;
     hsa_amd_memory_pool_t vram{};
     bool have_vram = false;
 };
@@ -297,11 +179,17 @@ hsa_status_t find_agent(hsa_agent_t a, void *p) {
         f->have_cpu = true;
     } else if (t == HSA_DEVICE_TYPE_GPU) {
         uint32_t bdf = 0, dom = 0;
+        char uuid[24] = {};
         hsa_agent_get_info(a, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_BDFID, &bdf);
         hsa_agent_get_info(a, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_DOMAIN, &dom);
-        if (bdf == f->bdf && dom == f->domain) {
-            f->gpu = a;
-            f->have_gpu = true;
+        if ((bdf & ~7u) == f->bdf && dom == f->domain) {
+            f->bdf_gpu = a;
+            ++f->bdf_matches;
+        }
+        if (f->have_uuid && hsa_agent_get_info(a, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_UUID, uuid) == HSA_STATUS_SUCCESS &&
+            !strncmp(uuid, "GPU-", 4) && !memcmp(uuid + 4, f->uuid, sizeof f->uuid)) {
+            f->uuid_gpu = a;
+            ++f->uuid_matches;
         }
     }
     return HSA_STATUS_SUCCESS;
@@ -378,17 +266,20 @@ void init_dev(int dev, DevState &d) {
     Find f;
     f.bdf = ((uint32_t)prop.pciBusID << 8) | ((uint32_t)prop.pciDeviceID << 3);
     f.domain = (uint32_t)prop.pciDomainID;
+    memcpy(f.uuid, prop.uuid.bytes, sizeof f.uuid);
+    for (char c : f.uuid) f.have_uuid |= c != 0;
     d.state = -2;
     if (hsa_init() != HSA_STATUS_SUCCESS) return;
     hsa_iterate_agents(find_agent, &f);
     d.state = -3;
-    if (!f.have_gpu || !f.have_cpu) return;
-    hsa_amd_agent_iterate_memory_pools(f.gpu, find_vram, &f);
+    if (!f.have_cpu || (f.uuid_matches != 1 && f.bdf_matches != 1)) return;
+    const hsa_agent_t gpu = f.uuid_matches == 1 ? f.uuid_gpu : f.bdf_gpu;
+    hsa_amd_agent_iterate_memory_pools(gpu, find_vram, &f);
     d.state = -4;
     if (!f.have_vram) return;
     d.state = -5;
     hsa_amd_hdp_flush_t hdp{};
-    if (hsa_agent_get_info(f.gpu, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_HDP_FLUSH, &hdp) != HSA_STATUS_SUCCESS ||
+    if (hsa_agent_get_info(gpu, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_HDP_FLUSH, &hdp) != HSA_STATUS_SUCCESS ||
         !hdp.HDP_MEM_FLUSH_CNTL)
         return;
     // code object
@@ -407,7 +298,7 @@ void init_dev(int dev, DevState &d) {
     if (hsa_code_object_reader_create_from_memory(co.data(), co.size(), &rd) != HSA_STATUS_SUCCESS) return;
     if (hsa_executable_create_alt(HSA_PROFILE_FULL, HSA_DEFAULT_FLOAT_ROUNDING_MODE_DEFAULT, nullptr, &exe) !=
             HSA_STATUS_SUCCESS ||
-        hsa_executable_load_agent_code_object(exe, f.gpu, rd, nullptr, nullptr) != HSA_STATUS_SUCCESS ||
+        hsa_executable_load_agent_code_object(exe, gpu, rd, nullptr, nullptr) != HSA_STATUS_SUCCESS ||
         hsa_executable_freeze(exe, nullptr) != HSA_STATUS_SUCCESS)
         return;     // (the reader and executable live as long as the process)
     d.state = -8;
@@ -421,7 +312,7 @@ void init_dev(int dev, DevState &d) {
                 hsa_executable_symbol_t s;
                 uint64_t ko = 0;
                 uint32_t kas = 0, lds = 1, priv = 1;
-                if (hsa_executable_get_symbol_by_name(exe, sym.c_str(), &f.gpu, &s) != HSA_STATUS_SUCCESS) continue;
+                if (hsa_executable_get_symbol_by_name(exe, sym.c_str(), &gpu, &s) != HSA_STATUS_SUCCESS) continue;
                 // the packets carry no LDS or scratch: a kernel that needs either
                 // (or reads arguments the host does not write) stays on the HIP path
                 if (hsa_executable_symbol_get_info(s, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_OBJECT, &ko) !=
@@ -449,39 +340,20 @@ void init_dev(int dev, DevState &d) {
         return;
     }
     d.state = -10;
-    if (hsa_queue_create(f.gpu, kQueueSize, HSA_QUEUE_TYPE_MULTI, queue_error_cb, &d, UINT32_MAX, UINT32_MAX,
+    if (hsa_queue_create(gpu, kQueueSize, HSA_QUEUE_TYPE_MULTI, queue_error_cb, &d, UINT32_MAX, UINT32_MAX,
                          &d.queue) != HSA_STATUS_SUCCESS) {
         hsa_amd_memory_pool_free(kp);
         return;
     }
-    d.agent = f.gpu;
-    if (timestamps()) hsa_amd_profiling_set_profiler_enabled(d.queue, 1);
-    // A/B only (tools/lazy_queues_ab.sh): idle queues that exist and are never used
-    if (const char *xq = getenv("MPIR_CVAR_REDUCE_LOCAL_DIRECT_IDLE_QUEUES")) {
-        for (int k = atoi(xq); k > 0 && k <= 8; --k) {
-            hsa_queue_t *q = nullptr;
-            (void)hsa_queue_create(f.gpu, 64, HSA_QUEUE_TYPE_MULTI, nullptr, nullptr, UINT32_MAX, UINT32_MAX, &q);
-        }
-    }
+    d.agent = gpu;
     if (!g_ts_freq) hsa_system_get_info(HSA_SYSTEM_INFO_TIMESTAMP_FREQUENCY, &g_ts_freq);
     d.karg = static_cast<char *>(kp);
     d.hdp = hdp.HDP_MEM_FLUSH_CNTL;
-    if (keepalive_us()) {
-        void *na = nullptr;
-        if (hsa_amd_memory_pool_allocate(f.vram, 256, 0, &na) == HSA_STATUS_SUCCESS &&
-            hsa_amd_agents_allow_access(1, &f.cpu, nullptr, na) == HSA_STATUS_SUCCESS) {
-            memset(na, 0, 256);      // LeanArgs {in, io, vbytes = 0, keep}: every workgroup returns at once
-            _mm_sfence();
-            *d.hdp = 1u;
-            (void)*d.hdp;
-            d.kargs_noop = static_cast<char *>(na);
-        }
-    }
     d.ok = true;
     d.state = 1;
 }
 
-// Every extra queue is created only when first needed: an idle queue that
+// The profiled queue is created only when first needed: an idle queue that
 // merely exists costs the calls' queue ~1 % at 64 MiB (the CP has one more
 // queue to serve; profiles/r02/keepalive_headline_ab.log, lazy_queues_ab.log).
 hsa_queue_t *profiled_queue(DevState &d) {
@@ -490,154 +362,25 @@ hsa_queue_t *profiled_queue(DevState &d) {
         if (hsa_queue_create(d.agent, kQueueSize, HSA_QUEUE_TYPE_MULTI, queue_error_cb, &d, UINT32_MAX, UINT32_MAX,
                              &q) != HSA_STATUS_SUCCESS)
             return;
-        // timestamps on from creation (see timestamps())
+        // timestamps on from creation (see kAcquireScope's comment above)
         hsa_amd_profiling_set_profiler_enabled(q, 1);
         d.pqueue = q;
     });
     return d.pqueue ? d.pqueue : d.queue;
 }
 
-bool keepalive_queue(DevState &d) {
-    std::call_once(d.konce, [&] {
-        if (!keepalive_own_queue()) {
-            d.kqueue = d.queue;
-        } else if (hsa_queue_create(d.agent, 64, HSA_QUEUE_TYPE_MULTI, queue_error_cb, &d, UINT32_MAX, UINT32_MAX,
-                                    &d.kqueue) != HSA_STATUS_SUCCESS) {
-            d.kqueue = nullptr;
-        }
-        d.kready.store(d.kqueue != nullptr);
-    });
-    return d.kready.load();
-}
-
-// ---- keep-alive thread (keepalive_us()) --------------------------------------
-std::atomic<bool> g_keepalive_stop{false};
-std::atomic<uint64_t> g_keepalive_packets{0}, g_keepalive_arms{0};
-std::once_flag g_keepalive_once;
-
-// one no-op packet on d.kqueue, no completion signal (under d.publish)
-void keepalive_packet(DevState &d) {
-    hsa_queue_t *q = d.kqueue;
-    const uint64_t idx = hsa_queue_load_write_index_relaxed(q);
-    if (idx - hsa_queue_load_read_index_scacquire(q) >= q->size) return;   // full: the CP is busy anyway
-    const uint64_t ko = d.kobj[0][MPIR_HIP_OP_SUM][MPIR_HIP_F32];
-    uint16_t header;
-    uint16_t setup = 0;
-    if (keepalive_kernel() && ko && d.kargs_noop) {
-        hsa_kernel_dispatch_packet_t *p = (hsa_kernel_dispatch_packet_t *)q->base_address + (idx & (q->size - 1));
-        memset((char *)p + 4, 0, sizeof(*p) - 4);
-        p->workgroup_size_x = kThreads;
-        p->workgroup_size_y = 1;
-        p->workgroup_size_z = 1;
-        p->grid_size_x = kThreads;
-        p->grid_size_y = 1;
-        p->grid_size_z = 1;
-        p->kernel_object = ko;
-        p->kernarg_address = d.kargs_noop;
-        header = (HSA_PACKET_TYPE_KERNEL_DISPATCH << HSA_PACKET_HEADER_TYPE) |
-                 (HSA_FENCE_SCOPE_NONE << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE) |
-                 (HSA_FENCE_SCOPE_NONE << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE);
-        setup = 1 << HSA_KERNEL_DISPATCH_PACKET_SETUP_DIMENSIONS;
-    } else {
-        hsa_barrier_and_packet_t *p = (hsa_barrier_and_packet_t *)q->base_address + (idx & (q->size - 1));
-        memset((char *)p + 4, 0, sizeof(*p) - 4);
-        header = (HSA_PACKET_TYPE_BARRIER_AND << HSA_PACKET_HEADER_TYPE) |
-                 (HSA_FENCE_SCOPE_NONE << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE) |
-                 (HSA_FENCE_SCOPE_NONE << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE);
-    }
-    hsa_queue_store_write_index_relaxed(q, idx + 1);
-    _mm_sfence();
-    __atomic_store_n((uint32_t *)((char *)q->base_address + (idx & (q->size - 1)) * 64),
-                     (uint32_t)header | ((uint32_t)setup << 16), __ATOMIC_RELEASE);
-    hsa_signal_store_screlease(q->doorbell_signal, idx);
-}
-
-// Keep the thread off the caller's core: pin it to the highest-numbered CPU of
-// its affinity mask other than the one the arming call ran on (a napping thread
-// free to share the spinning caller's core cost it 2-6 %, ka_isolate.log).
-void keepalive_pin(int caller_cpu) {
-    if (getenv("MPIR_CVAR_REDUCE_LOCAL_KEEPALIVE_NOPIN")) return;   // A/B only
-    cpu_set_t set;
-    if (sched_getaffinity(0, sizeof set, &set) != 0) return;
-    for (int c = CPU_SETSIZE - 1; c >= 0; --c) {
-        if (c == caller_cpu || !CPU_ISSET(c, &set)) continue;
-        cpu_set_t one;
-        CPU_ZERO(&one);
-        CPU_SET(c, &one);
-        (void)pthread_setaffinity_np(pthread_self(), sizeof one, &one);
-        return;
-    }
-}
-
-void keepalive_loop(int caller_cpu) {
-    keepalive_pin(caller_cpu);
-    if (getenv("MPIR_CVAR_REDUCE_LOCAL_KEEPALIVE_EMPTY")) {   // A/B only: a thread that only naps
-        const timespec ms = {0, 1000000};
-        while (!g_keepalive_stop.load(std::memory_order_relaxed)) nanosleep(&ms, nullptr);
-        return;
-    }
-    prctl(PR_SET_TIMERSLACK, 1000UL);     // 1 us: nanosleep wakes near the period
-    // (no SCHED_IDLE: with it, the napping thread alone cost bench.py's
-    // spinning caller 4-21 %, profiles/r02/ka_isolate.log)
-    const uint64_t period = (uint64_t)keepalive_us() * 1000ull;
-    // naps: half a period while some device idles inside its window (a packet
-    // goes out at most 1.5 periods after the last one), a whole period while a
-    // call is in flight (the CP is busy; fewer wake-ups for back-to-back
-    // callers), 1 ms once every window has expired
-    const timespec nap = {0, (long)(period / 2)}, busy_nap = {0, (long)period}, idle_nap = {0, 1000000};
-    int state = 1;    // 0 nothing in its window, 1 idle in its window, 2 a call in flight
-    while (!g_keepalive_stop.load(std::memory_order_relaxed)) {
-        nanosleep(state == 0 ? &idle_nap : state == 2 ? &busy_nap : &nap, nullptr);
-        const uint64_t t = mono_ns();
-        bool active = false, busy = false;
-        for (int i = 0; i < kMaxDirectDev; ++i) {
-            DevState &d = g_dev[i];
-            if (!d.ok || !d.kready.load(std::memory_order_acquire) || d.queue_error.load(std::memory_order_relaxed))
-                continue;
-            // (signed: a call may have stamped a time after this thread read the clock)
-            const uint64_t lc = d.last_call_ns.load(std::memory_order_relaxed);
-            if (!d.armed.load(std::memory_order_relaxed) || !lc || (int64_t)(t - lc) > (int64_t)keepalive_active_ns())
-                continue;
-            active = true;
-            const uint64_t last = d.last_packet_ns.load(std::memory_order_relaxed);
-            if (d.call_busy.load(std::memory_order_relaxed)) {
-                busy = true;
-                continue;
-            }
-            if ((int64_t)(t - last) < (int64_t)period) continue;
-            std::lock_guard<std::mutex> lk(d.publish);
-            if (g_keepalive_stop.load(std::memory_order_relaxed)) return;
-            // re-check under the lock: a call that published meanwhile is in flight
-            if (d.call_busy.load(std::memory_order_relaxed) ||
-                (int64_t)(mono_ns() - d.last_packet_ns.load(std::memory_order_relaxed)) < (int64_t)period)
-                continue;
-            keepalive_packet(d);
-            g_keepalive_packets.fetch_add(1, std::memory_order_relaxed);
-            d.last_packet_ns.store(mono_ns(), std::memory_order_relaxed);
-        }
-        state = !active ? 0 : busy ? 2 : 1;
-    }
-}
-
-// at exit, before the HIP / HSA runtimes tear down (registered after they
-// initialised, so it runs first): no packet after this returns
-void keepalive_stop() {
-    g_keepalive_stop.store(true);
-    if (getenv("MPIR_CVAR_REDUCE_LOCAL_KEEPALIVE_DEBUG"))
-        fprintf(stderr, "mpir_hip keep-alive: %llu arms, %llu packets\n",
-                (unsigned long long)g_keepalive_arms.load(), (unsigned long long)g_keepalive_packets.load());
-    for (int i = 0; i < kMaxDirectDev; ++i) {
-        if (!g_dev[i].ok) continue;
-        std::lock_guard<std::mutex> lk(g_dev[i].publish);
-    }
-}
-
-void keepalive_start() {
-    if (getenv("MPIR_CVAR_REDUCE_LOCAL_KEEPALIVE_NOTHREAD")) return;   // A/B only
-    std::call_once(g_keepalive_once, [] {
-        atexit(keepalive_stop);
-        std::thread(keepalive_loop, sched_getcpu()).detach();
-    });
+// AQL rings in VRAM by default.  ROCm places every queue's ring in host memory
+// unless HSA_ALLOCATE_QUEUE_DEV_MEM=1; with the ring in VRAM the CP fetches each
+// dispatch packet locally, 1.4 us off every synchronous call
+// (profiles/r02/sync_ab_ring.log), and HIP's own queues gain the same.  The HSA
+// runtime reads the variable once, when it starts, and hsa_queue_create takes no
+// per-queue choice in this ROCm; so the library sets the default when it is
+// loaded -- before main() for a program linked against it (libmpi in Option 1),
+// before the first HIP call for one that loads it first -- and leaves any value
+// the environment already holds (HSA_ALLOCATE_QUEUE_DEV_MEM=0 keeps ROCm's
+// placement).  Loaded after the HSA runtime started, it changes nothing.
+__attribute__((constructor)) void default_rings_in_vram() {
+    setenv("HSA_ALLOCATE_QUEUE_DEV_MEM", "1", 0);
 }
 
 }  // namespace
@@ -665,12 +408,9 @@ struct DirectSignals {
             if (!have[dev]) {
                 // The host polls the signal and never sleeps on it, so it needs no
                 // interrupt event: naming the GPU as its only consumer makes ROCr
-                // create a plain memory signal (MPIR_CVAR_REDUCE_LOCAL_DIRECT_SIGNAL
-                // =interrupt keeps the default, event-backed kind)
-                hsa_status_t st;
-                if (signal_kind() == 0) st = hsa_signal_create(0, 1, &g_dev[dev].agent, &sig[dev]);
-                else st = hsa_signal_create(0, 0, nullptr, &sig[dev]);
-                if (st != HSA_STATUS_SUCCESS) return false;
+                // create a plain memory signal (an event-backed one measured the
+                // same, profiles/r02/sync_ab_ring.log)
+                if (hsa_signal_create(0, 1, &g_dev[dev].agent, &sig[dev]) != HSA_STATUS_SUCCESS) return false;
                 have[dev] = true;
             }
         }
@@ -697,23 +437,6 @@ int direct_reduce(int dev, int op, int elem, const ReducePlan &p, int *rc) {
     DevState &d = g_dev[dev];
     std::call_once(d.once, [&] { init_dev(dev, d); });
     if (!d.ok || d.queue_error.load(std::memory_order_relaxed)) return 0;
-    if (keepalive_us()) {
-        // arm on a call after a gap, disarm on a back-to-back one
-        const uint64_t lc = d.last_call_ns.load(std::memory_order_relaxed);
-        if (lc) {
-            const int64_t gap = (int64_t)(mono_ns() - lc);
-            const int64_t p = (int64_t)keepalive_us() * 1000;
-            if (gap > p + 10000) {
-                if (!d.armed.load(std::memory_order_relaxed) && keepalive_queue(d)) {
-                    d.armed.store(1, std::memory_order_relaxed);
-                    g_keepalive_arms.fetch_add(1, std::memory_order_relaxed);
-                    keepalive_start();
-                }
-            } else if (gap < p && d.armed.load(std::memory_order_relaxed)) {
-                d.armed.store(0, std::memory_order_relaxed);
-            }
-        }
-    }
     const uint64_t ko = d.kobj[p.kind][op][elem];
     // the packet's grid_size_x (workgroups x kThreads) is 32 bits
     if (!ko || p.groups == 0 || p.groups > (uint64_t)UINT32_MAX / kThreads) return 0;
@@ -781,6 +504,7 @@ int direct_reduce(int dev, int op, int elem, const ReducePlan &p, int *rc) {
             _mm_sfence();
             *d.hdp = 1u;        // HDP flush: the BAR writes land in VRAM before the CP reads them
             (void)*d.hdp;
+            g_kernarg_writes.fetch_add(1, std::memory_order_relaxed);
         }
         hsa_queue_t *q = prof ? profiled_queue(d) : d.queue;
         const uint64_t idx = hsa_queue_load_write_index_relaxed(q);
@@ -797,8 +521,8 @@ int direct_reduce(int dev, int op, int elem, const ReducePlan &p, int *rc) {
         p->kernarg_address = slot;
         p->completion_signal = sig;
         const uint16_t header = (HSA_PACKET_TYPE_KERNEL_DISPATCH << HSA_PACKET_HEADER_TYPE) |
-                                (acquire_scope() << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE) |
-                                (release_scope() << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE);
+                                (kAcquireScope << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE) |
+                                (kReleaseScope << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE);
         const uint16_t setup = 1 << HSA_KERNEL_DISPATCH_PACKET_SETUP_DIMENSIONS;
         hsa_queue_store_write_index_relaxed(q, idx + 1);
         // the ring may be write-combined VRAM (HSA_ALLOCATE_QUEUE_DEV_MEM): the
@@ -807,9 +531,7 @@ int direct_reduce(int dev, int op, int elem, const ReducePlan &p, int *rc) {
         __atomic_store_n((uint32_t *)p, (uint32_t)header | ((uint32_t)setup << 16), __ATOMIC_RELEASE);
         if (prof) th1 = sys_ts();
         hsa_signal_store_screlease(q->doorbell_signal, idx);
-        if (keepalive_us()) d.call_busy.store(1, std::memory_order_relaxed);
     }
-    if (use_mwaitx() && !d.queue_error.load(std::memory_order_relaxed)) wait_signal_mwaitx(sig);
     for (uint64_t it = 1; hsa_signal_load_scacquire(sig) != 0; ++it) {
         if ((it & 0xFFFF) == 0 && d.queue_error.load(std::memory_order_relaxed)) {
             *rc = MPIR_HIP_ERUNTIME;
@@ -819,14 +541,6 @@ int direct_reduce(int dev, int op, int elem, const ReducePlan &p, int *rc) {
     }
     if (held) held->inflight.fetch_sub(1, std::memory_order_acq_rel);
     if (ring >= 0) d.ring_busy[ring].store(0, std::memory_order_release);
-    if (keepalive_us()) {
-        // (with several threads calling, one's end may clear another's busy
-        // flag: at worst a keep-alive packet goes out during a call, harmless)
-        const uint64_t t = mono_ns();
-        d.last_packet_ns.store(t, std::memory_order_relaxed);
-        d.last_call_ns.store(t, std::memory_order_relaxed);
-        d.call_busy.store(0, std::memory_order_relaxed);
-    }
     if (prof) {
         const uint64_t th2 = sys_ts();
         hsa_amd_profiling_dispatch_time_t t{};
@@ -861,5 +575,7 @@ int direct_state(int dev) {
 }
 
 uint64_t direct_busy_skips() { return g_busy_skips.load(std::memory_order_relaxed); }
+
+uint64_t direct_kernarg_writes() { return g_kernarg_writes.load(std::memory_order_relaxed); }
 
 }  // namespace mpir_hip

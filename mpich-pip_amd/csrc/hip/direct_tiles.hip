@@ -23,9 +23,7 @@ using namespace mpir_hip;
 #define MPIR_DIRECT_TILE(OPN, OP, E, T)                                                                   \
     extern "C" __global__ __launch_bounds__(kThreads) void mpir_tile_##OPN##_##E(const char *in, char *io, \
                                                                                  uint64_t vbytes, uint64_t keep) { \
-        const uint64_t base = (uint64_t)blockIdx.x * kTileBytes;                                          \
-        if (base >= vbytes) return;                                                                       \
-        reduce_tile<OP, T>(in, io, base, vbytes, keep);                                                   \
+        reduce_tile<OP, T>(in, io, blockIdx.x, vbytes, keep);                                             \
     }                                                                                                     \
     extern "C" __global__ __launch_bounds__(kThreads) void mpir_tilex_##OPN##_##E(TileArgs<T> a) {       \
         reduce_tile_body<OP, T>(a);                                                                       \

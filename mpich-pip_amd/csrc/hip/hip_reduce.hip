@@ -37,12 +37,13 @@ uint64_t direct_last_kernel_ns();
 int direct_state(int dev);
 void direct_last_split(uint64_t out[4]);
 uint64_t direct_busy_skips();
+uint64_t direct_kernarg_writes();
 Entry g_table[MPIR_HIP_NOPS][MPIR_HIP_NELEMS];
 multi_fn g_multi[MPIR_HIP_NOPS][MPIR_HIP_NELEMS][2][3];
 
-// Bytes at the end of each result stored sc1 (into the Infinity Cache) rather
-// than nt: MPIR_CVAR_REDUCE_LOCAL_KEEP_MB (0 = every store nt), default 64
-// (reduce_kernels.hpp, kKeepBytes).
+// Results of at most this many bytes are stored sc1 (into the Infinity Cache)
+// rather than nt: MPIR_CVAR_REDUCE_LOCAL_KEEP_MB (0 = every store nt), default
+// 64 (reduce_kernels.hpp, kKeepBytes).
 uint64_t keep_bytes() {
     static const uint64_t v = [] {
         const char *e = getenv("MPIR_CVAR_REDUCE_LOCAL_KEEP_MB");
@@ -53,16 +54,7 @@ uint64_t keep_bytes() {
     return v;
 }
 
-uint64_t keep_for(uint64_t vbytes) {
-    // MPIR_CVAR_REDUCE_LOCAL_KEEP_MODE: "whole" (default) or "tail" (reduce_kernels.hpp)
-    static const bool tail = [] {
-        const char *e = getenv("MPIR_CVAR_REDUCE_LOCAL_KEEP_MODE");
-        return e && !strcmp(e, "tail");
-    }();
-    const uint64_t k = keep_bytes();
-    if (tail) return k;
-    return vbytes <= k ? vbytes : 0;
-}
+uint64_t keep_for(uint64_t vbytes) { return vbytes <= keep_bytes() ? vbytes : 0; }
 }  // namespace mpir_hip
 
 namespace {
@@ -591,6 +583,8 @@ int MPIR_Hip_direct_state(int dev) { return direct_state(dev); }
 void MPIR_Hip_direct_last_split(uint64_t out[4]) { direct_last_split(out); }
 
 uint64_t MPIR_Hip_direct_busy_skips(void) { return direct_busy_skips(); }
+
+uint64_t MPIR_Hip_direct_kernarg_writes(void) { return direct_kernarg_writes(); }
 
 int MPIR_Hip_thread_contexts(void) {
     std::lock_guard<std::mutex> lk(g_pool_mu);

@@ -14,9 +14,10 @@
 //     by ILP + 8 waves/CU of TLP), with a one-instruction issue gap after
 //     each (inout, in) pair (issue_gap below: 0.810 -> 0.830-0.841 of peak);
 //   * buffer_load/store_dwordx4 with the `nt` cache policy (aux = 2) on both
-//     operands and on the store (sc1 on the stores of the last 64 MiB of a
-//     result, which stay in the Infinity Cache: kKeepBytes below):
-//     streamed-once data should not displace L2 / Infinity Cache lines; measured 0.81 of the 8 TB/s HBM peak vs 0.70 for
+//     operands and on the store (a result of at most 64 MiB is stored sc1
+//     instead, so it stays in the Infinity Cache for its next reader:
+//     kKeepBytes below): streamed-once data should not displace L2 / Infinity
+//     Cache lines; measured 0.81 of the 8 TB/s HBM peak vs 0.70 for
 //     default-policy loads and 0.63 for a grid-stride loop (before the gap);
 //   * the buffer descriptor covers exactly this tile's bytes, so the ragged
 //     last tile needs no branch: out-of-range loads return 0 and out-of-range
@@ -45,11 +46,10 @@ constexpr int kCachePolicySC1 = 16;                           // aux bit: sc1 (d
 // traffic 27.0 vs 33.2 us (tools/sync_store_ab.hip,
 // profiles/r01s4_sync_store_ab.log).  With nothing re-read the two policies
 // are within noise at <= 64 MiB, and at 256 MiB sc1 on any part of the result
-// costs ~1 us (profiles/r02/pairs_ab.log: the "last 64 MiB sc1" variant,
-// MPIR_CVAR_REDUCE_LOCAL_KEEP_MODE=tail, only won where the bench's own
-// rotation let the next call but three re-read that tail from the MALL).
-// The kernels take the per-call `keep` and store sc1 the tiles in the last
-// `keep` bytes: keep = vbytes (all), 0 (none), or the tail mode's 64 MiB.
+// costs ~1 us (profiles/r02/pairs_ab.log: a "last 64 MiB sc1" variant only won
+// where the bench's own rotation let the next call but three re-read that tail
+// from the MALL; withdrawn).  The kernels take the per-call `keep` and store
+// sc1 the tiles in the last `keep` bytes: keep = vbytes (all) or 0 (none).
 // Nothing else changes: the bytes reach HBM either way (MALL is memory-side).
 constexpr uint64_t kKeepBytes = 64ull << 20;
 uint64_t keep_bytes();               // MPIR_CVAR_REDUCE_LOCAL_KEEP_MB (hip_reduce.hip)
@@ -128,16 +128,44 @@ __device__ __forceinline__ void issue_gap() {
     __builtin_amdgcn_sched_barrier(0);
 }
 
-// One 16 KiB tile per operand: each wave owns a contiguous 4 KiB of it (one
-// 1 KiB lane-contiguous access per instruction).
+// The tile grid sits on kTileBytes boundaries of inoutbuf's ADDRESS, not of
+// its start: tile t covers [t * kTileBytes - s, (t + 1) * kTileBytes - s) of the
+// vector region, s = io mod kTileBytes, clipped to [0, vbytes).  Operands that
+// start off a 16 KiB boundary otherwise put every tile across two 16 KiB
+// blocks, every wave's 4 KiB across two 4 KiB blocks (and at 64 B off, every
+// 1 KiB access across nine 128 B lines instead of eight): measured at 256 MiB
+// (tools/align_sweep.py, profiles/r03/align_sweep.log), both operands 64 B /
+// 4 KiB / 8 KiB off a 2 MiB boundary took 125.0 / 124.0 / 128.5 us against
+// 120.8 us aligned.  Tile 0 is then the partial block up to the first
+// boundary: its lanes below the cut get offsets that wrap past the buffer
+// descriptor's range (loads return 0, stores are dropped), like the lanes past
+// the end of the last tile.  `in` shares io's offset mod 16 (tile_split), not
+// necessarily mod 16 KiB.
+__device__ __forceinline__ uint32_t tile_shift(const void *io) {
+    return (uint32_t)(reinterpret_cast<uintptr_t>(io) & (kTileBytes - 1));
+}
+
+// workgroups of the tile grid over a vector region of vbytes at io
+__host__ __device__ inline uint64_t tile_groups(const void *io, uint64_t vbytes) {
+    const uint64_t s = reinterpret_cast<uintptr_t>(io) & (kTileBytes - 1);
+    const uint64_t g = (vbytes + s + kTileBytes - 1) / kTileBytes;
+    return g ? g : 1;
+}
+
+// Tile `tile` of the grid: each wave owns a contiguous 4 KiB of it (one 1 KiB
+// lane-contiguous access per instruction).
 template <class Op, class T>
-__device__ __forceinline__ void reduce_tile(const char *in, char *io, uint64_t base, uint64_t vbytes, uint64_t keepb) {
-    const uint64_t left = vbytes - base;
-    const int nrec = (int)(left < kTileBytes ? left : kTileBytes);
-    __amdgpu_buffer_rsrc_t rin = __builtin_amdgcn_make_buffer_rsrc((void *)(in + base), 0, nrec, 0x00020000);
-    __amdgpu_buffer_rsrc_t rio = __builtin_amdgcn_make_buffer_rsrc((void *)(io + base), 0, nrec, 0x00020000);
+__device__ __forceinline__ void reduce_tile(const char *in, char *io, uint64_t tile, uint64_t vbytes, uint64_t keepb) {
+    const int64_t start = (int64_t)(tile * kTileBytes) - (int64_t)tile_shift(io);
+    const uint64_t lo = start > 0 ? (uint64_t)start : 0;
+    if (lo >= vbytes) return;
+    const uint64_t end = (uint64_t)(start + kTileBytes);
+    const int nrec = (int)((end < vbytes ? end : vbytes) - lo);
+    const int cut = (int)(lo - start);       // 0, or s for tile 0: lanes below it wrap out of range
+    __amdgpu_buffer_rsrc_t rin = __builtin_amdgcn_make_buffer_rsrc((void *)(in + lo), 0, nrec, 0x00020000);
+    __amdgpu_buffer_rsrc_t rio = __builtin_amdgcn_make_buffer_rsrc((void *)(io + lo), 0, nrec, 0x00020000);
     const int t = (int)threadIdx.x;
-    const int wb = (t >> 6) * (kVecPerLane * 1024) + (t & 63) * 16;
+    const int wb = (t >> 6) * (kVecPerLane * 1024) + (t & 63) * 16 - cut;
     u32x4 a[kVecPerLane], b[kVecPerLane];
 #pragma unroll
     for (int u = 0; u < kVecPerLane; ++u) {
@@ -145,7 +173,7 @@ __device__ __forceinline__ void reduce_tile(const char *in, char *io, uint64_t b
         b[u] = __builtin_amdgcn_raw_buffer_load_b128(rin, wb + u * 1024, 0, kCachePolicyNT);
         if (u + 1 < kVecPerLane) issue_gap();
     }
-    const bool keep = keep_tile(base, vbytes, keepb);
+    const bool keep = keep_tile(lo, vbytes, keepb);
 #pragma unroll
     for (int u = 0; u < kVecPerLane; ++u) store16(combine16<Op, T>(a[u], b[u]), rio, wb + u * 1024, keep);
 }
@@ -154,8 +182,7 @@ __device__ __forceinline__ void reduce_tile(const char *in, char *io, uint64_t b
 // after its tile.
 template <class Op, class T>
 __device__ __forceinline__ void reduce_tile_body(const TileArgs<T> &args) {
-    const uint64_t base = (uint64_t)blockIdx.x * kTileBytes;
-    if (base < args.vbytes) reduce_tile<Op, T>(args.in, args.io, base, args.vbytes, args.keep);
+    reduce_tile<Op, T>(args.in, args.io, blockIdx.x, args.vbytes, args.keep);
     if (blockIdx.x == 0) {
         Op op;
         const unsigned t = threadIdx.x;
@@ -173,9 +200,7 @@ __global__ __launch_bounds__(kThreads) void k_reduce_tile(TileArgs<T> args) {
 // 16): four scalar arguments and nothing after the tile.
 template <class Op, class T>
 __global__ __launch_bounds__(kThreads) void k_reduce_tile_lean(const char *in, char *io, uint64_t vbytes, uint64_t keep) {
-    const uint64_t base = (uint64_t)blockIdx.x * kTileBytes;
-    if (base >= vbytes) return;
-    reduce_tile<Op, T>(in, io, base, vbytes, keep);
+    reduce_tile<Op, T>(in, io, blockIdx.x, vbytes, keep);
 }
 
 // inbuf misaligned relative to inoutbuf: (in - io) mod 16 = delta != 0, the
@@ -371,8 +396,7 @@ void plan_reduce(const void *in_, void *io_, uint64_t count, ReducePlan &p) {
     TileArgs<T> ta;
     __builtin_memset(&ta, 0, sizeof ta);
     if (tile_split<T>(in_, io_, count, ta)) {
-        p.groups = (ta.vbytes + kTileBytes - 1) / kTileBytes;
-        if (p.groups == 0) p.groups = 1;
+        p.groups = tile_groups(ta.io, ta.vbytes);
         if (ta.nhead || ta.ntail) {
             p.kind = kPlanFull;
             __builtin_memcpy(p.args, &ta, sizeof ta);

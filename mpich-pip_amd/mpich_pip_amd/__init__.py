@@ -121,7 +121,7 @@ EXPORTED_SYMBOLS = [
     "MPIR_Hip_memcpy", "MPIR_Hip_error_string", "MPIR_Hip_device_count", "MPIR_Hip_thread_contexts",
     "MPIR_Hip_host_max_bytes", "MPIR_Hip_set_host_max_bytes", "MPIR_Hip_mixed_max_bytes", "MPIR_Hip_direct_dispatches", "MPIR_Hip_direct_profile",
     "MPIR_Hip_direct_last_kernel_ns", "MPIR_Hip_direct_state", "MPIR_Hip_direct_busy_skips",
-    "MPIR_Hip_direct_last_split",
+    "MPIR_Hip_direct_last_split", "MPIR_Hip_direct_kernarg_writes",
     # runtime subset for config 1 (include/mpi_pip.h)
     "MPI_Init", "MPI_Initialized", "MPI_Finalize", "MPI_Finalized", "MPI_Abort", "MPI_Comm_size",
     "MPI_Comm_rank", "MPI_Get_processor_name", "MPI_Wtime", "MPI_Wtick", "MPI_Barrier", "MPI_Bcast",
@@ -200,6 +200,7 @@ def load(path: str | None = None) -> ctypes.CDLL:
     lib.MPIR_Hip_direct_state.argtypes = [i32]
     lib.MPIR_Hip_direct_state.restype = i32
     lib.MPIR_Hip_direct_busy_skips.restype = ctypes.c_uint64
+    lib.MPIR_Hip_direct_kernarg_writes.restype = ctypes.c_uint64
     lib.MPIR_Hip_direct_last_split.argtypes = [ctypes.POINTER(ctypes.c_uint64)]
     lib.MPIR_Hip_direct_last_split.restype = None
     lib.MPIR_Hip_error_string.restype = ctypes.c_char_p

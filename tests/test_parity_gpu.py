@@ -920,6 +920,34 @@ def test_direct_dispatch_many_threads_distinct_windows(mpi, cuda):
             assert np.array_equal(da[k][w].cpu().numpy(), want[w]), (k, w)
 
 
+def test_direct_dispatch_fresh_args_every_call(mpi, cuda):
+    """Every call with new kernel arguments (a window shifted by 256 B each
+    time, 1500 calls over 1024 distinct argument sets): each misses the kernarg
+    cache, so its arguments are written into a VRAM slot that earlier
+    dispatches read (128 cache slots, each rewritten ~10 times) and made
+    visible by the HDP flush before the doorbell.  A stale read would combine
+    the wrong window: each element's final value counts exactly the calls whose
+    window covered it, checked against numpy's replay of the same sequence."""
+    torch = cuda
+    n, nbuf, noff, calls = 4096, 4, 256, 1500
+    span = n + noff * 64
+    da = [torch.zeros(span, dtype=torch.float32, device="cuda") for _ in range(nbuf)]
+    db = [torch.ones(span, dtype=torch.float32, device="cuda") for _ in range(nbuf)]
+    torch.cuda.synchronize()
+    f = mpi.fast_reduce_local()
+    lib = mpi.load()
+    w0, d0 = lib.MPIR_Hip_direct_kernarg_writes(), _direct_count(mpi)
+    want = [np.zeros(span, np.float32) for _ in range(nbuf)]
+    for i in range(calls):
+        j, o = i % nbuf, ((i // nbuf) * 37) % noff * 64          # element offsets, 256 B steps
+        assert f(db[j].data_ptr() + 4 * o, da[j].data_ptr() + 4 * o, n, mpi.MPI_FLOAT, mpi.MPI_SUM) == 0
+        want[j][o:o + n] += 1
+    assert _direct_count(mpi) - d0 == calls
+    assert lib.MPIR_Hip_direct_kernarg_writes() - w0 >= calls - 2 * nbuf
+    for j in range(nbuf):
+        assert np.array_equal(da[j].cpu().numpy(), want[j]), j
+
+
 def test_direct_dispatch_orders_after_null_stream(mpi, cuda):
     """Work the caller left running on the legacy null stream for the operands
     is finished before the reduction reads them: the direct path first

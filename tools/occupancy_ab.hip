@@ -28,7 +28,7 @@ extern "C" __global__ __launch_bounds__(kThreads) void occ_tile(const char *in, 
     const uint64_t base = (uint64_t)blockIdx.x * kTileBytes;
     if (base >= vbytes) return;
     if (vbytes == 1) reserve[threadIdx.x] = 0;   // never true: keeps the reservation referenced
-    reduce_tile<OpSum, float>(in, io, base, vbytes, 0);
+    reduce_tile<OpSum, float>(in, io, blockIdx.x, vbytes, 0);
 }
 
 int main(int argc, char **argv) {

@@ -35,14 +35,14 @@ using namespace mpir_hip;
 
 template <int G>
 __global__ __launch_bounds__(256) void k_stride(const char *in, char *io, uint64_t vbytes, uint32_t ntiles) {
-    for (uint32_t t = blockIdx.x; t < ntiles; t += G) reduce_tile<OpSum, float>(in, io, (uint64_t)t * kTileBytes, vbytes, 0);
+    for (uint32_t t = blockIdx.x; t < ntiles; t += G) reduce_tile<OpSum, float>(in, io, (uint64_t)t, vbytes, 0);
 }
 
 template <int G>
 __global__ __launch_bounds__(256) void k_chunk(const char *in, char *io, uint64_t vbytes, uint32_t ntiles) {
     const uint32_t per = (ntiles + G - 1) / G;
     const uint32_t b = blockIdx.x * per, e = min(ntiles, b + per);
-    for (uint32_t t = b; t < e; ++t) reduce_tile<OpSum, float>(in, io, (uint64_t)t * kTileBytes, vbytes, 0);
+    for (uint32_t t = b; t < e; ++t) reduce_tile<OpSum, float>(in, io, (uint64_t)t, vbytes, 0);
 }
 
 // ctr: this launch's 8 counters (64 B apart); other: the next launch's, zeroed here
@@ -62,7 +62,7 @@ __global__ __launch_bounds__(256) void k_ticket(const char *in, char *io, uint64
 #pragma unroll 1
         for (int k = 0; k < T; ++k) {
             const uint32_t t = ticket * T + k;
-            if (t < ntiles) reduce_tile<OpSum, float>(in, io, (uint64_t)t * kTileBytes, vbytes, 0);
+            if (t < ntiles) reduce_tile<OpSum, float>(in, io, (uint64_t)t, vbytes, 0);
         }
         __syncthreads();
         j = next_s;
