@@ -80,7 +80,7 @@ def parse():
                          "itself through torch.distributed.run before any GPU call")
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=50,
-                    help="untimed calls first: the GPU clocks and the kernarg cache settle (profiles/r02/warmup_ab.log)")
+                    help="untimed calls first: the GPU clocks and the kernarg cache settle (profiles/archive/r02/warmup_ab.log)")
     ap.add_argument("--mib", type=int, default=256, help="MiB per operand (metric: 256)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="only the timed MPI_Reduce_local loop")
@@ -736,7 +736,7 @@ def main():
             rc = lib.MPI_Reduce_local(pb.ctypes.data, pa.ctypes.data, count, m.MPI_FLOAT, m.MPI_SUM)
             assert rc == 0
         # both-host calls take the host combine by default (it beats the PCIe
-        # round trip at every size, profiles/r02/host_crossover.log); the
+        # round trip at every size, profiles/archive/r02/host_crossover.log); the
         # staging pipeline is forced here with a host limit of 0 so that the
         # PCIe-inclusive rate of the GPU path stays measured
         prev = lib.MPIR_Hip_set_host_max_bytes(0)

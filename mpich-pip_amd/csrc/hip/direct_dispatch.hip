@@ -3,7 +3,7 @@
 // code object (direct_tiles.hip -> lib/libmpir_hip_tiles.hsaco), kernargs in
 // VRAM, and a wait on the dispatch packet's own completion signal.
 //
-// Why (tools/aql/aql2.cpp, profiles/r02/aql2_*.log): a synchronous HIP call
+// Why (tools/aql/aql2.cpp, profiles/archive/r02/aql2_*.log): a synchronous HIP call
 // is hipLaunchKernel + a completion word written by hipStreamWriteValue32,
 // which is a second (blit) dispatch; the GPU then sits idle 8.8-8.9 us between
 // one call's last workgroup and the next call's first.  A direct dispatch
@@ -12,7 +12,7 @@
 // kernel); with the kernarg cache below and the AQL rings in VRAM
 // (HSA_ALLOCATE_QUEUE_DEV_MEM=1, the library's default: default_rings_in_vram)
 // the gap is 5.2-5.5 us, 4.3 us of it the CP
-// noticing the doorbell (profiles/r02/sync_split_timeline.log, cp_latency.log).  An earlier attempt (round 1) lost because its kernargs sat in host
+// noticing the doorbell (profiles/archive/r02/sync_split_timeline.log, cp_latency.log).  An earlier attempt (round 1) lost because its kernargs sat in host
 // memory (every workgroup read them over PCIe); here they are written through
 // the BAR into VRAM and made visible with an HDP flush (the register ROCr
 // exposes as HSA_AMD_AGENT_INFO_HDP_FLUSH; read back, as HIP does for its
@@ -49,6 +49,7 @@
 #include <string.h>
 #include <pthread.h>
 #include <time.h>
+#include <unistd.h>
 
 #include <atomic>
 #include <mutex>
@@ -63,30 +64,50 @@ namespace mpir_hip {
 namespace {
 
 constexpr int kMaxDirectDev = 64;
-constexpr uint32_t kKargSlots = 256, kKargSlotBytes = 128;
-// Kernarg slots 0..kRingSlots-1 are a ring for one-off arguments; the rest are
-// a direct-mapped cache: a call whose (kernel, arguments) match a cached slot
-// dispatches with that slot as it stands -- no BAR write and no HDP flush
-// (0.95 us of host time per dispatch with its read-back, tools/aql/aql2.cpp,
-// profiles/r02/aql2_host_costs.log).  A reduction schedule that calls again on
-// the same buffers, or a caller rotating a few buffer pairs, hits.  A cached
-// slot is rewritten only when no dispatch that uses it is in flight.
-constexpr uint32_t kRingSlots = 128, kCacheSlots = kKargSlots - kRingSlots;
+constexpr uint32_t kKargSlotBytes = sizeof(KargSlot);
+static_assert(kKargSlotBytes == 128, "one kernarg slot per 128-byte L2 line");
+// Kernarg slots, by region: [0, kRingSlots) a ring for one-off arguments;
+// [kRingSlots, +kCacheSlots) a direct-mapped cache: a call whose (kernel,
+// arguments) match a cached slot that a checked dispatch has read back
+// complete dispatches the unchecked kernel with that slot as it stands, no
+// host write at all; [kProfBase, +kRingSlots) the ring of the
+// timestamped twin queue, whose dispatch ids count separately (a slot is only
+// ever stamped by one queue's packets).  A reduction schedule that calls
+// again on the same buffers, or a caller rotating a few buffer pairs, hits.  A
+// cached slot's arguments are rewritten only when no dispatch that uses it
+// is in flight.
+//
+// Every other call writes its slot through the BAR (KargSlot's layout,
+// reduce_kernels.hpp) and dispatches the checked kernel: the argument words
+// that change, an sfence, each half's nonce (the packet's queue index + 1), an
+// sfence, then an HDP flush -- without reading the flush register back, the
+// PCIe round trip that cost every kernarg-cache miss ~1 us before its doorbell
+// (1.7 us from entry to doorbell on a miss against 0.35 us on a hit,
+// profiles/r03/fresh_args_split_before_grid.log).  Correctness does not rest on
+// the flush's timing: the checked kernels (direct_tiles.hip checked_args)
+// re-read a slot whose halves carry a nonce older than their dispatch id + 1,
+// so a workgroup never combines with stale arguments.
+constexpr uint32_t kRingSlots = 128, kCacheSlots = 128, kProfBase = kRingSlots + kCacheSlots;
+constexpr uint32_t kKargSlots = kProfBase + kRingSlots;
 constexpr uint32_t kQueueSize = 256;
 
 // a plan's argument bytes (LeanArgs / TileArgs / ShiftArgs / ElemsArgs,
 // reduce_kernels.hpp; their layouts do not depend on the element type)
 constexpr uint32_t kMaxArgBytes = sizeof(ReducePlan::args);
-static_assert(kMaxArgBytes <= kKargSlotBytes, "kernarg slot too small");
+static_assert(kMaxArgBytes <= kSlotArgBytes, "kernarg slot too small");
 constexpr uint32_t kPlanArgBytes[kPlanKinds] = {sizeof(LeanArgs), sizeof(TileArgs<char>), sizeof(ShiftArgs<char>),
                                                 sizeof(ElemsArgs), sizeof(ElemsArgs)};
-const char *const kPlanPrefix[kPlanKinds] = {"mpir_tile_", "mpir_tilex_", "mpir_tiles_", "mpir_elems_", "mpir_elemsu_"};
+// per plan kind, the unchecked and the checked kernel (direct_tiles.hip)
+const char *const kPlanPrefix[2][kPlanKinds] = {
+    {"mpir_tile_", "mpir_tilex_", "mpir_tiles_", "mpir_elems_", "mpir_elemsu_"},
+    {"mpir_ctile_", "mpir_ctilex_", "mpir_ctiles_", "mpir_celems_", "mpir_celemsu_"}};
 
 struct CacheEntry {
-    uint64_t ko = 0;
+    uint64_t ko = 0;                            // the unchecked kernel of the plan
     uint32_t n = 0;                             // argument bytes
     alignas(8) unsigned char args[kMaxArgBytes] = {};
     std::atomic<int> inflight{0};
+    std::atomic<int> verified{0};               // a checked dispatch read this write complete
 };
 
 struct DevState {
@@ -98,11 +119,12 @@ struct DevState {
     hsa_queue_t *pqueue = nullptr;              // the same, timestamps on: calls while profiling is on
     std::once_flag ponce;                       // (created at the first profiled call)
     char *karg = nullptr;                       // kKargSlots x kKargSlotBytes, VRAM, host-written
-    uint32_t kslot = 0;                         // next ring slot to try (under `publish`)
-    std::atomic<int> ring_busy[kRingSlots] = {};  // a ring slot's dispatch is in flight
+    volatile uint32_t *err = nullptr;           // host memory: a kernel found its arguments missing
+    uint32_t kslot = 0, pslot = 0;              // next ring / profiled-ring slot to try (under `publish`)
+    std::atomic<int> ring_busy[2 * kRingSlots] = {};  // a (profiled) ring slot's dispatch is in flight
     CacheEntry cache[kCacheSlots];
     volatile uint32_t *hdp = nullptr;
-    uint64_t kobj[kPlanKinds][MPIR_HIP_NOPS][MPIR_HIP_NELEMS] = {};   // by plan kind (kPlanPrefix)
+    uint64_t kobj[2][kPlanKinds][MPIR_HIP_NOPS][MPIR_HIP_NELEMS] = {};   // [checked][plan kind] (kPlanPrefix)
     std::mutex publish;
     std::atomic<int> queue_error{0};
 };
@@ -137,7 +159,7 @@ int mode() {
 
 // The calls' queue records no dispatch timestamps: with them the CP's
 // per-packet timestamp writes cost the synchronous call ~0.4 us at 256 MiB and
-// ~0.9 us at 64 MiB (alternated processes, tools/ts_ab.sh, profiles/r02/ts_ab.log),
+// ~0.9 us at 64 MiB (alternated processes, tools/ts_ab.sh, profiles/archive/r02/ts_ab.log),
 // and switching them on for a live queue does not take effect
 // (tools/ts_enable_probe.py).  A second queue, created with them on, takes the
 // calls made while MPIR_Hip_direct_profile is on (the bench's roofline readout:
@@ -147,7 +169,7 @@ int mode() {
 // system-scope acquire costs ~7 us of kernel body, aql_sig_nt_sys) and
 // system-scope release, so the result is visible to every agent -- SDMA copies
 // and the host included -- when the signal fires.  Other scopes measured within
-// 0.2 us (tools/scope_ab.sh, profiles/r02/scope_ab.log); none at release would
+// 0.2 us (tools/scope_ab.sh, profiles/archive/r02/scope_ab.log); none at release would
 // leave results in one XCD's L2 and is not offered.
 constexpr int kAcquireScope = HSA_FENCE_SCOPE_AGENT;
 constexpr int kReleaseScope = HSA_FENCE_SCOPE_SYSTEM;
@@ -306,9 +328,10 @@ void init_dev(int dev, DevState &d) {
     for (int op = 1; op < MPIR_HIP_NOPS; ++op) {
         for (int e = 1; e < MPIR_HIP_NELEMS; ++e) {
             if (!op_name(op) || !elem_name(e)) continue;
-            // every plan kind, each with the argument size the host writes
-            for (int kind = 0; kind < kPlanKinds; ++kind) {
-                const std::string sym = std::string(kPlanPrefix[kind]) + op_name(op) + "_" + elem_name(e) + ".kd";
+            // every plan kind, unchecked and checked, each taking one kernarg slot
+            for (int kc = 0; kc < 2 * kPlanKinds; ++kc) {
+                const int chk = kc / kPlanKinds, kind = kc % kPlanKinds;
+                const std::string sym = std::string(kPlanPrefix[chk][kind]) + op_name(op) + "_" + elem_name(e) + ".kd";
                 hsa_executable_symbol_t s;
                 uint64_t ko = 0;
                 uint32_t kas = 0, lds = 1, priv = 1;
@@ -323,9 +346,9 @@ void init_dev(int dev, DevState &d) {
                         HSA_STATUS_SUCCESS ||
                     hsa_executable_symbol_get_info(s, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_PRIVATE_SEGMENT_SIZE, &priv) !=
                         HSA_STATUS_SUCCESS ||
-                    kas != kPlanArgBytes[kind] || lds != 0 || priv != 0)
+                    kas != kKargSlotBytes || lds != 0 || priv != 0)
                     continue;
-                d.kobj[kind][op][e] = ko;
+                d.kobj[chk][kind][op][e] = ko;
                 ++found;
             }
         }
@@ -347,15 +370,38 @@ void init_dev(int dev, DevState &d) {
     }
     d.agent = gpu;
     if (!g_ts_freq) hsa_system_get_info(HSA_SYSTEM_INFO_TIMESTAMP_FREQUENCY, &g_ts_freq);
+    // the kernels' error word: fine-grained host memory the GPU can write
+    d.state = -11;
+    void *ew = nullptr;
+    if (hipHostMalloc(&ew, 64, hipHostMallocCoherent | hipHostMallocMapped | hipHostMallocPortable) != hipSuccess) {
+        (void)hipGetLastError();
+        hsa_queue_destroy(d.queue);
+        d.queue = nullptr;
+        hsa_amd_memory_pool_free(kp);
+        return;
+    }
+    d.err = static_cast<volatile uint32_t *>(ew);
+    *d.err = 0;
     d.karg = static_cast<char *>(kp);
     d.hdp = hdp.HDP_MEM_FLUSH_CNTL;
+    // Every slot starts with the error word's address (the same in every later
+    // write, so never stale) and nonce 0, below every dispatch id + 1; this
+    // once, the flush is read back.
+    {
+        KargSlot init{};
+        init.w[6] = (uint64_t)(uintptr_t)ew;
+        for (uint32_t k = 0; k < kKargSlots; ++k) memcpy(d.karg + (size_t)k * kKargSlotBytes, &init, sizeof init);
+        _mm_sfence();
+        *d.hdp = 1u;
+        (void)*d.hdp;
+    }
     d.ok = true;
     d.state = 1;
 }
 
 // The profiled queue is created only when first needed: an idle queue that
 // merely exists costs the calls' queue ~1 % at 64 MiB (the CP has one more
-// queue to serve; profiles/r02/keepalive_headline_ab.log, lazy_queues_ab.log).
+// queue to serve; profiles/archive/r02/keepalive_headline_ab.log, lazy_queues_ab.log).
 hsa_queue_t *profiled_queue(DevState &d) {
     std::call_once(d.ponce, [&] {
         hsa_queue_t *q = nullptr;
@@ -372,7 +418,7 @@ hsa_queue_t *profiled_queue(DevState &d) {
 // AQL rings in VRAM by default.  ROCm places every queue's ring in host memory
 // unless HSA_ALLOCATE_QUEUE_DEV_MEM=1; with the ring in VRAM the CP fetches each
 // dispatch packet locally, 1.4 us off every synchronous call
-// (profiles/r02/sync_ab_ring.log), and HIP's own queues gain the same.  The HSA
+// (profiles/archive/r02/sync_ab_ring.log), and HIP's own queues gain the same.  The HSA
 // runtime reads the variable once, when it starts, and hsa_queue_create takes no
 // per-queue choice in this ROCm; so the library sets the default when it is
 // loaded -- before main() for a program linked against it (libmpi in Option 1),
@@ -409,7 +455,7 @@ struct DirectSignals {
                 // The host polls the signal and never sleeps on it, so it needs no
                 // interrupt event: naming the GPU as its only consumer makes ROCr
                 // create a plain memory signal (an event-backed one measured the
-                // same, profiles/r02/sync_ab_ring.log)
+                // same, profiles/archive/r02/sync_ab_ring.log)
                 if (hsa_signal_create(0, 1, &g_dev[dev].agent, &sig[dev]) != HSA_STATUS_SUCCESS) return false;
                 have[dev] = true;
             }
@@ -437,9 +483,9 @@ int direct_reduce(int dev, int op, int elem, const ReducePlan &p, int *rc) {
     DevState &d = g_dev[dev];
     std::call_once(d.once, [&] { init_dev(dev, d); });
     if (!d.ok || d.queue_error.load(std::memory_order_relaxed)) return 0;
-    const uint64_t ko = d.kobj[p.kind][op][elem];
+    const uint64_t ko = d.kobj[0][p.kind][op][elem], ko_checked = d.kobj[1][p.kind][op][elem];
     // the packet's grid_size_x (workgroups x kThreads) is 32 bits
-    if (!ko || p.groups == 0 || p.groups > (uint64_t)UINT32_MAX / kThreads) return 0;
+    if (!ko || !ko_checked || p.groups == 0 || p.groups > (uint64_t)UINT32_MAX / kThreads) return 0;
     // Work queued on the legacy null stream stays ordered before us, as it is
     // for the HIP path's blocking library stream.  hipStreamQuery(nullptr)
     // keeps answering "not ready" after such work has finished until the host
@@ -462,53 +508,79 @@ int direct_reduce(int dev, int op, int elem, const ReducePlan &p, int *rc) {
     hsa_signal_store_relaxed(sig, 1);
     CacheEntry *held = nullptr;
     int ring = -1;
+    bool checked = true;
     {
         std::lock_guard<std::mutex> lk(d.publish);
-        uint64_t h = ko;
-        for (uint32_t w = 0; w < kn / 8; ++w) {
-            uint64_t x;
-            memcpy(&x, ka + 8 * w, 8);
-            h = (h ^ x) * 0x9E3779B97F4A7C15ull;
-        }
-        h ^= h >> 29;
-        const uint32_t ci = (uint32_t)(h % kCacheSlots);
-        CacheEntry &e = d.cache[ci];
-        char *slot;
-        const bool hit = e.ko == ko && e.n == kn && !memcmp(e.args, ka, kn);
-        if (hit || e.inflight.load(std::memory_order_acquire) == 0) {
-            slot = d.karg + (size_t)(kRingSlots + ci) * kKargSlotBytes;
-            e.inflight.fetch_add(1, std::memory_order_acq_rel);
-            held = &e;
-            if (!hit) {
-                e.ko = ko;
-                e.n = kn;
-                memcpy(e.args, ka, kn);
-            }
-        } else {
-            // a ring slot no in-flight dispatch reads (workgroups load their
-            // kernargs when they start, i.e. all through a long kernel's life)
-            for (uint32_t k = 0; k < kRingSlots; ++k) {
-                const uint32_t r = (d.kslot + k) % kRingSlots;
-                if (d.ring_busy[r].load(std::memory_order_acquire) == 0) {
-                    ring = (int)r;
-                    break;
-                }
-            }
-            if (ring < 0) return 0;     // every ring slot in flight: the HIP path takes this call
-            d.kslot = (uint32_t)ring + 1;
-            d.ring_busy[ring].store(1, std::memory_order_relaxed);
-            slot = d.karg + (size_t)ring * kKargSlotBytes;
-        }
-        if (!hit) {
-            memcpy(slot, ka, kn);
-            _mm_sfence();
-            *d.hdp = 1u;        // HDP flush: the BAR writes land in VRAM before the CP reads them
-            (void)*d.hdp;
-            g_kernarg_writes.fetch_add(1, std::memory_order_relaxed);
-        }
         hsa_queue_t *q = prof ? profiled_queue(d) : d.queue;
         const uint64_t idx = hsa_queue_load_write_index_relaxed(q);
         while (idx - hsa_queue_load_read_index_scacquire(q) >= q->size) _mm_pause();
+        char *slot = nullptr;
+        bool write_args = true;
+        // a free slot of a ring (first slot `base` of d.karg, busy flags from `busy`)
+        auto take_ring = [&](uint32_t base, uint32_t busy, uint32_t &next) -> bool {
+            for (uint32_t k = 0; k < kRingSlots; ++k) {
+                const uint32_t r = (next + k) % kRingSlots;
+                if (d.ring_busy[busy + r].load(std::memory_order_acquire) == 0) {
+                    ring = (int)(busy + r);
+                    next = r + 1;
+                    d.ring_busy[ring].store(1, std::memory_order_relaxed);
+                    slot = d.karg + (size_t)(base + r) * kKargSlotBytes;
+                    return true;
+                }
+            }
+            return false;
+        };
+        if (prof) {
+            if (!take_ring(kProfBase, kRingSlots, d.pslot)) return 0;
+        } else {
+            uint64_t h = ko;
+            for (uint32_t w = 0; w < kn / 8; ++w) {
+                uint64_t x;
+                memcpy(&x, ka + 8 * w, 8);
+                h = (h ^ x) * 0x9E3779B97F4A7C15ull;
+            }
+            h ^= h >> 29;
+            const uint32_t ci = (uint32_t)(h % kCacheSlots);
+            CacheEntry &e = d.cache[ci];
+            const bool hit = e.ko == ko && e.n == kn && !memcmp(e.args, ka, kn);
+            if (hit || e.inflight.load(std::memory_order_acquire) == 0) {
+                slot = d.karg + (size_t)(kRingSlots + ci) * kKargSlotBytes;
+                e.inflight.fetch_add(1, std::memory_order_acq_rel);
+                held = &e;
+                if (hit) {
+                    write_args = false;
+                    // read back complete by an earlier checked dispatch: as it stands
+                    checked = !e.verified.load(std::memory_order_acquire);
+                } else {
+                    e.verified.store(0, std::memory_order_relaxed);
+                    e.ko = ko;
+                    e.n = kn;
+                    memcpy(e.args, ka, kn);
+                }
+            } else if (!take_ring(0, 0, d.kslot)) {
+                return 0;       // every ring slot in flight: the HIP path takes this call
+            }
+        }
+        if (checked) {
+            // the argument words that change, then each half's nonce (KargSlot);
+            // the sfences order them on PCIe, so a half showing the nonce holds
+            // its words
+            uint64_t *ks = reinterpret_cast<uint64_t *>(slot);
+            if (write_args) {
+                uint64_t w[12] = {};
+                memcpy(w, ka, kn);
+                for (int i = 0; i < 6; ++i) {
+                    ks[i] = w[i];
+                    ks[8 + i] = w[6 + i];
+                }
+                _mm_sfence();
+                g_kernarg_writes.fetch_add(1, std::memory_order_relaxed);
+            }
+            ks[7] = idx + 1;
+            ks[15] = idx + 1;
+            _mm_sfence();
+            *d.hdp = 1u;        // HDP flush, not read back (see kRingSlots)
+        }
         hsa_kernel_dispatch_packet_t *p = (hsa_kernel_dispatch_packet_t *)q->base_address + (idx & (q->size - 1));
         memset((char *)p + 4, 0, sizeof(*p) - 4);
         p->workgroup_size_x = kThreads;
@@ -517,7 +589,7 @@ int direct_reduce(int dev, int op, int elem, const ReducePlan &p, int *rc) {
         p->grid_size_x = groups * kThreads;
         p->grid_size_y = 1;
         p->grid_size_z = 1;
-        p->kernel_object = ko;
+        p->kernel_object = checked ? ko_checked : ko;
         p->kernarg_address = slot;
         p->completion_signal = sig;
         const uint16_t header = (HSA_PACKET_TYPE_KERNEL_DISPATCH << HSA_PACKET_HEADER_TYPE) |
@@ -539,7 +611,20 @@ int direct_reduce(int dev, int op, int elem, const ReducePlan &p, int *rc) {
         }
         _mm_pause();
     }
-    if (held) held->inflight.fetch_sub(1, std::memory_order_acq_rel);
+    if (__builtin_expect(*d.err != 0, 0)) {
+        // a workgroup never saw its arguments land (direct_tiles.hip
+        // checked_args) and combined nothing: this call fails, and the path is
+        // closed (the slot stays held)
+        d.queue_error.store(-2, std::memory_order_relaxed);
+        *rc = MPIR_HIP_ERUNTIME;
+        return 1;
+    }
+    if (held) {
+        // every workgroup of a checked dispatch saw the write: later hits on the
+        // entry may take the unchecked kernel
+        if (checked) held->verified.store(1, std::memory_order_release);
+        held->inflight.fetch_sub(1, std::memory_order_acq_rel);
+    }
     if (ring >= 0) d.ring_busy[ring].store(0, std::memory_order_release);
     if (prof) {
         const uint64_t th2 = sys_ts();

@@ -5,40 +5,139 @@
 // launch_reduce (reg<Op, T> in the reg_*.hip units: every op on the integer,
 // real, complex, pair and x87 classes; not the 32-byte classes or REPLACE) --
 // one per kind of plan_reduce's launch plan (reduce_kernels.hpp), under plain
-// names the host looks up:
-//   mpir_tile_<op>_<elem>    k_reduce_tile_lean's body (LeanArgs, 32 B):
+// names the host looks up, each taking one 128-byte kernarg slot and each in
+// an unchecked and a checked form (below):
+//   mpir_tile_<op>_<elem>    k_reduce_tile_lean's body (LeanArgs):
 //                            16 B-aligned operands of 16 B multiples;
-//   mpir_tilex_<op>_<elem>   k_reduce_tile's body (TileArgs, 80 B): equal
+//   mpir_tilex_<op>_<elem>   k_reduce_tile's body (TileArgs): equal
 //                            alignment mod 16, head / tail elements by
 //                            workgroup 0;
-//   mpir_tiles_<op>_<elem>   k_reduce_shift's body (ShiftArgs, 96 B): unequal
+//   mpir_tiles_<op>_<elem>   k_reduce_shift's body (ShiftArgs): unequal
 //                            alignment mod 16, two tiles or more;
 //   mpir_elems_<op>_<elem>   k_reduce_elems<NATURAL = true / false> (ElemsArgs,
-//   mpir_elemsu_<op>_<elem>  32 B, the grid stride an argument): the rest.
+//   mpir_elemsu_<op>_<elem>  the grid stride an argument): the rest.
 // None reads a hidden argument (no gridDim), so a bare AQL packet launches it.
 #include "kernel_table.hpp"
 
 using namespace mpir_hip;
 
-#define MPIR_DIRECT_TILE(OPN, OP, E, T)                                                                   \
-    extern "C" __global__ __launch_bounds__(kThreads) void mpir_tile_##OPN##_##E(const char *in, char *io, \
-                                                                                 uint64_t vbytes, uint64_t keep) { \
-        reduce_tile<OP, T>(in, io, blockIdx.x, vbytes, keep);                                             \
-    }                                                                                                     \
-    extern "C" __global__ __launch_bounds__(kThreads) void mpir_tilex_##OPN##_##E(TileArgs<T> a) {       \
-        reduce_tile_body<OP, T>(a);                                                                       \
-    }                                                                                                     \
-    extern "C" __global__ __launch_bounds__(kThreads) void mpir_tiles_##OPN##_##E(ShiftArgs<T> a) {      \
-        reduce_shift_body<OP, T>(a);                                                                      \
-    }                                                                                                     \
-    extern "C" __global__ __launch_bounds__(kThreads) void mpir_elems_##OPN##_##E(                       \
-        const char *in, char *io, uint64_t n, uint64_t stride) {                                          \
-        reduce_elems<OP, T, true>(in, io, n, stride);                                                     \
-    }                                                                                                     \
-    extern "C" __global__ __launch_bounds__(kThreads) void mpir_elemsu_##OPN##_##E(                      \
-        const char *in, char *io, uint64_t n, uint64_t stride) {                                          \
-        reduce_elems<OP, T, false>(in, io, n, stride);                                                    \
+// Every kernel takes one 128-byte kernarg slot (KargSlot, reduce_kernels.hpp):
+// the plan's argument bytes in words 0-5 and 8-13, the device's error word in
+// word 6, a nonce in words 7 and 15 (one copy per 64-byte half).  Each plan
+// kind comes twice:
+//   mpir_<kind>_*    reads its arguments as they stand.  The host dispatches
+//                    it on a kernarg-cache hit whose slot an earlier, checked
+//                    dispatch has already read back complete: nothing is
+//                    written for the call.
+//   mpir_c<kind>_*   checked.  The host wrote the slot for this call through
+//                    the BAR -- the argument words, an sfence, the nonce (the
+//                    packet's queue index + 1, which the CP hands every wave
+//                    as its dispatch id), an HDP flush -- and rang the doorbell
+//                    WITHOUT reading the flush register back (a ~1 us PCIe
+//                    round trip).  A workgroup accepts its slot when the
+//                    halves holding its arguments carry a nonce >= its dispatch
+//                    id + 1 (a later dispatch of the same arguments may have
+//                    re-stamped the slot meanwhile); one whose kernarg fetch
+//                    beat the BAR writes to memory sees an older nonce and
+//                    re-reads past the caches until the write lands.  The CP's
+//                    ~4 us from doorbell to dispatch makes that a safety net;
+//                    if the nonce never arrives (10 ms) the workgroup touches
+//                    nothing and sets the error word, and the call fails
+//                    instead of combining stale arguments.
+// Measured against round 2's single protocol (tools/aql/kslot_ab.cpp,
+// interleaved call by call, profiles/r03/kslot_ab.log): checking on every call
+// cost hits ~1.2 us (the heavier prologue and the per-call stamp), so hits stay
+// unchecked.
+
+// the dispatch id (SGPRs the CP fills from the packet's queue index; clang
+// exposes the LLVM intrinsic without a builtin)
+extern "C" __device__ uint64_t mpir_dispatch_id(void) __asm("llvm.amdgcn.dispatch.id");
+
+template <class A>
+constexpr bool kTwoHalves = sizeof(A) > 48;     // words 0-5 hold 48 bytes
+
+template <class A>
+__device__ __forceinline__ void unpack_args(const KargSlot &s, A *a) {
+    static_assert(sizeof(A) <= kSlotArgBytes, "plan arguments exceed the kernarg slot");
+    uint64_t words[12];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+        words[i] = s.w[i];
+        words[6 + i] = s.w[8 + i];
     }
+    __builtin_memcpy(a, words, sizeof(A));
+}
+
+template <class A>
+__device__ __forceinline__ bool slot_fresh(const KargSlot &s, uint64_t want) {
+    return s.w[7] >= want && (!kTwoHalves<A> || s.w[15] >= want);
+}
+
+// checked: the slot's arguments once they carry this dispatch's nonce, or false
+// (error word set) when they never arrived
+template <class A>
+__device__ __forceinline__ bool checked_args(KargSlot s, A *a) {
+    const uint64_t want = mpir_dispatch_id() + 1;
+    // the words in registers before the check, in one statement: the loads
+    // issue together and cost one scalar round trip, as a plain argument load
+    if constexpr (kTwoHalves<A>)
+        asm volatile("" : "+s"(s.w[0]), "+s"(s.w[1]), "+s"(s.w[2]), "+s"(s.w[3]), "+s"(s.w[4]), "+s"(s.w[5]),
+                     "+s"(s.w[7]), "+s"(s.w[8]), "+s"(s.w[9]), "+s"(s.w[10]), "+s"(s.w[11]), "+s"(s.w[12]),
+                     "+s"(s.w[13]), "+s"(s.w[15]));
+    else
+        asm volatile("" : "+s"(s.w[0]), "+s"(s.w[1]), "+s"(s.w[2]), "+s"(s.w[3]), "+s"(s.w[7]));
+    if (__builtin_expect(!slot_fresh<A>(s, want), 0)) {
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();      // 100 MHz
+        const uint64_t *g = (const uint64_t *)(uintptr_t)__builtin_amdgcn_kernarg_segment_ptr();
+        bool ok = false;
+        while (!ok) {
+            __builtin_amdgcn_s_sleep(2);
+            __builtin_amdgcn_s_dcache_inv();
+            asm volatile("buffer_inv sc0 sc1" ::: "memory");
+            for (int i = 0; i < 16; ++i) s.w[i] = __builtin_nontemporal_load(g + i);
+            ok = slot_fresh<A>(s, want);
+            if (!ok && __builtin_amdgcn_s_memrealtime() - t0 > 1000000) {   // 10 ms: never landed
+                if (threadIdx.x == 0)
+                    __hip_atomic_store(reinterpret_cast<uint32_t *>(s.w[6]), 1u, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_SYSTEM);
+                return false;
+            }
+        }
+    }
+    unpack_args(s, a);
+    return true;
+}
+
+template <class A>
+__device__ __forceinline__ bool plain_args(const KargSlot &s, A *a) {
+    unpack_args(s, a);
+    return true;
+}
+
+#define MPIR_DIRECT_KIND(PFX, GET, OPN, OP, E, T)                                                         \
+    extern "C" __global__ __launch_bounds__(kThreads) void mpir_##PFX##tile_##OPN##_##E(KargSlot ks) {   \
+        LeanArgs a;                                                                                       \
+        if (GET(ks, &a)) reduce_tile<OP, T>(a.in, a.io, blockIdx.x, a.vbytes, a.keep);                    \
+    }                                                                                                     \
+    extern "C" __global__ __launch_bounds__(kThreads) void mpir_##PFX##tilex_##OPN##_##E(KargSlot ks) {  \
+        TileArgs<T> a;                                                                                    \
+        if (GET(ks, &a)) reduce_tile_body<OP, T>(a);                                                      \
+    }                                                                                                     \
+    extern "C" __global__ __launch_bounds__(kThreads) void mpir_##PFX##tiles_##OPN##_##E(KargSlot ks) {  \
+        ShiftArgs<T> a;                                                                                   \
+        if (GET(ks, &a)) reduce_shift_body<OP, T>(a);                                                     \
+    }                                                                                                     \
+    extern "C" __global__ __launch_bounds__(kThreads) void mpir_##PFX##elems_##OPN##_##E(KargSlot ks) {  \
+        ElemsArgs a;                                                                                      \
+        if (GET(ks, &a)) reduce_elems<OP, T, true>(a.in, a.io, a.n, a.stride);                            \
+    }                                                                                                     \
+    extern "C" __global__ __launch_bounds__(kThreads) void mpir_##PFX##elemsu_##OPN##_##E(KargSlot ks) { \
+        ElemsArgs a;                                                                                      \
+        if (GET(ks, &a)) reduce_elems<OP, T, false>(a.in, a.io, a.n, a.stride);                           \
+    }
+
+#define MPIR_DIRECT_TILE(OPN, OP, E, T) MPIR_DIRECT_KIND(, plain_args, OPN, OP, E, T) \
+                                        MPIR_DIRECT_KIND(c, checked_args, OPN, OP, E, T)
 
 // the (op, class) matrix of reg_sum_prod / reg_max_min / reg_logic / reg_pairs_x87
 #define X(E, T) MPIR_DIRECT_TILE(SUM, OpSum, E, T) MPIR_DIRECT_TILE(PROD, OpProd, E, T)

@@ -75,7 +75,7 @@ constexpr int kMaxStageSlots = 8;
 // transfers run at the same time (PCIe is full duplex).  Events order the
 // stages of one chunk and stop a slot from being refilled before its
 // copy-back has read it.  Defaults 16 MiB x 3 slots (tools/stage_sweep.py,
-// profiles/r01s3_stage_sweep.log: pinned 71.8 GiB/s, pageable 66.3 with the
+// profiles/archive/r01s3_stage_sweep.log: pinned 71.8 GiB/s, pageable 66.3 with the
 // bounce path below; 32 MiB chunks leave a longer tail of copy-outs).
 // MPIR_CVAR_REDUCE_LOCAL_STAGE_CHUNK_MB / MPIR_CVAR_REDUCE_LOCAL_STAGE_SLOTS override.
 // (function-local statics: initialised once, thread-safe)
@@ -218,7 +218,7 @@ int get_bounce(int dev, size_t bytes, char **out) {
 // Host copies of the bounce path, split over a small process-wide pool of
 // worker threads: one thread moves 31-33 GB/s between pageable and pinned
 // memory on the MI355X host, four 83-86 GB/s (tools/memcpy_bw.cpp,
-// profiles/r01s3_memcpy_bw.log) -- more than the ~51 GB/s a PCIe Gen5 x16
+// profiles/archive/r01s3_memcpy_bw.log) -- more than the ~51 GB/s a PCIe Gen5 x16
 // upload takes; the host combine uses every thread (copy_pool() below).
 // MPIR_CVAR_REDUCE_LOCAL_STAGE_THREADS (1 = the calling thread alone).  The pool is never torn down: its idle workers end
 // with the process, so exit never waits on them.
@@ -258,7 +258,7 @@ class CopyPool {
     }
     // copies split into at most copy_n_ parts: PCIe, not the host's memory,
     // bounds them, and more parts only add wake-ups (host->device 1 MiB 52 ->
-    // 74 us with 16 parts, profiles/r02/host_threads_ab.log)
+    // 74 us with 16 parts, profiles/archive/r02/host_threads_ab.log)
     void copy(char *dst, const char *src, size_t bytes, size_t min_split = (size_t)1 << 20) {
         if (copy_n_ <= 1 || bytes < min_split || getpid() != pid_) {
             memcpy(dst, src, bytes);
@@ -322,7 +322,7 @@ int usable_cpus() {
 // Default pool size: the usable CPUs, 4 to 16, for the host combine of large
 // both-host operands, which is memory-bound and scales with threads (256 MiB
 // fp32 SUM on the MI355X host, 16-CPU quota: 131-136 GiB/s on 4 threads,
-// 259-299 on 16; profiles/r02/host_threads_ab.log).  Copies (bounce path,
+// 259-299 on 16; profiles/archive/r02/host_threads_ab.log).  Copies (bounce path,
 // mixed-residency slots) keep to 4 parts, which already outrun a PCIe upload.
 // MPIR_CVAR_REDUCE_LOCAL_STAGE_THREADS sets both.
 CopyPool &copy_pool() {
@@ -345,7 +345,7 @@ enum Loc { LOC_HOST = 0, LOC_DEVICE = 1, LOC_PINNED = 2 };
 // the copy pool's threads from host_split_bytes()) instead of a staged GPU
 // round trip -- SURVEY.md §8b's dispatch rule ("both host -> CPU").  Measured
 // on the MI355X host, fp32 SUM (tools/host_latency.py, tools/host_crossover.py,
-// profiles/r02/host_latency*.log, host_crossover.log): the host combine wins at
+// profiles/archive/r02/host_latency*.log, host_crossover.log): the host combine wins at
 // every size -- 0.4 us against 48 us staged at 4 B, 35 against 125-194 us at
 // 1 MiB, 108 against 299-466 us at 4 MiB, 5.6-5.7 against 10.7-13.9 ms at 256 MiB
 // (staging is PCIe-bound, ~50 GB/s up).  MPIR_CVAR_REDUCE_LOCAL_HOST_MAX_KB:
@@ -363,7 +363,7 @@ uint64_t host_max_bytes() { return g_host_max.load(std::memory_order_relaxed); }
 // the host operand is copied into a pinned, device-mapped slot and the kernel
 // reads (and for a host inoutbuf writes) it there over PCIe -- one dispatch, no
 // DMA copies, no staging pipeline.  Measured fp32 SUM host -> device at count 1:
-// 33 us through the staged pipeline (profiles/r02/host_latency.log).
+// 33 us through the staged pipeline (profiles/archive/r02/host_latency.log).
 // MPIR_CVAR_REDUCE_LOCAL_MIXED_MAX_KB (default 1024; 0 = always stage).
 uint64_t mixed_max_bytes() {
     static const uint64_t v = [] {
@@ -377,7 +377,7 @@ uint64_t mixed_max_bytes() {
 // copies into / out of the mixed path's slot of at least this many bytes go
 // through the copy pool (MPIR_CVAR_REDUCE_LOCAL_MIXED_SPLIT_KB, default 512: the
 // pool's wake-up costs ~10 us, more than it saves at 256 KiB, less at 1 MiB --
-// device -> host 135 -> 72-85 us; profiles/r02/mixed_split_ab.log)
+// device -> host 135 -> 72-85 us; profiles/archive/r02/mixed_split_ab.log)
 size_t zc_split_bytes() {
     static const size_t v = [] {
         const char *e = getenv("MPIR_CVAR_REDUCE_LOCAL_MIXED_SPLIT_KB");
@@ -447,7 +447,7 @@ int device_count() {
 // the host reads it only after that work, the ordering the device path keeps
 // for device operands (direct_reduce) and the blocking library streams keep for
 // staged ones.  hipStreamQuery(NULL) keeps answering "not ready" for finished
-// work until the host synchronises (profiles/r02/direct_probe.log), so "not
+// work until the host synchronises (profiles/archive/r02/direct_probe.log), so "not
 // ready" is followed by hipStreamSynchronize(NULL).  Pageable operands need
 // nothing: HIP's copies into pageable memory complete before they return.
 int order_after_null_stream() {

@@ -44,9 +44,9 @@ constexpr int kCachePolicySC1 = 16;                           // aux bit: sc1 (d
 // stays there for its next reader (the next schedule step, the RCCL send of a
 // block, the D2H copy of a staged chunk): 64 MiB re-read within ~256 MiB of
 // traffic 27.0 vs 33.2 us (tools/sync_store_ab.hip,
-// profiles/r01s4_sync_store_ab.log).  With nothing re-read the two policies
+// profiles/archive/r01s4_sync_store_ab.log).  With nothing re-read the two policies
 // are within noise at <= 64 MiB, and at 256 MiB sc1 on any part of the result
-// costs ~1 us (profiles/r02/pairs_ab.log: a "last 64 MiB sc1" variant only won
+// costs ~1 us (profiles/archive/r02/pairs_ab.log: a "last 64 MiB sc1" variant only won
 // where the bench's own rotation let the next call but three re-read that tail
 // from the MALL; withdrawn).  The kernels take the per-call `keep` and store
 // sc1 the tiles in the last `keep` bytes: keep = vbytes (all) or 0 (none).
@@ -120,7 +120,7 @@ __device__ __forceinline__ u32x4 combine16(u32x4 a, u32x4 b) {
 // every (inout, in) pair of 16 B loads.  rocprofv3 kernel trace, 256 MiB fp32
 // SUM, same tile otherwise: 119.7 us (0.841 of the HBM peak) vs 124.2 us
 // (0.810) with the eight loads back to back (tools/shape_ab.hip,
-// profiles/r01s3_shape_ab.log); a gap after every load, or s_nop 3, measured
+// profiles/archive/r01s3_shape_ab.log); a gap after every load, or s_nop 3, measured
 // the same, s_nop 7 less.
 __device__ __forceinline__ void issue_gap() {
     __builtin_amdgcn_sched_barrier(0);
@@ -383,6 +383,16 @@ struct ReducePlan {
     alignas(16) unsigned char args[sizeof(ShiftArgs<char>)];
 };
 
+// The direct AQL dispatch's kernarg slot (direct_dispatch.hip writes it,
+// direct_tiles.hip's kernels read it): one 128-byte L2 line, two 64-byte halves.
+//   words 0-5, 8-13   the plan's argument bytes (at most kSlotArgBytes)
+//   word 6            address of the device's error word (host memory)
+//   words 7, 15       the nonce, one copy per half: the queue index + 1 of the
+//                     last packet that stamped the slot (its dispatch id + 1)
+struct KargSlot { uint64_t w[16]; };
+constexpr uint32_t kSlotArgBytes = 96;
+static_assert(sizeof(ShiftArgs<char>) <= kSlotArgBytes, "ShiftArgs must fit the kernarg slot");
+
 // Fills `p` (padding bytes zero: the direct path's kernarg cache compares bytes).
 template <class T>
 void plan_reduce(const void *in_, void *io_, uint64_t count, ReducePlan &p) {
@@ -494,7 +504,7 @@ hipError_t launch_reduce(const void *in, void *io, uint64_t count, hipStream_t s
 // (fully coalesced buffer_load/store_dwordx4 nt, like k_reduce_tile), staged
 // through LDS, and each lane combines whole elements out of LDS -- the soft
 // x87 combine needs an element's two 16-byte halves in one lane.  Measured at
-// 256 MiB (profiles/r01_kernel_ab_wide_lds.log): SUM 0.78, MAXLOC 0.81 of the
+// 256 MiB (profiles/archive/r01_kernel_ab_wide_lds.log): SUM 0.78, MAXLOC 0.81 of the
 // HBM peak vs 0.65 when each lane loads its own halves (lanes 32 B apart, every
 // 128-byte line fetched twice under `nt`).  The buffer range check handles
 // the ragged last tile (zeros in, stores dropped).
@@ -813,7 +823,7 @@ hipError_t launch_combine_any(const void *const *ins, int n, int tree, void *out
 
 template <class Op, class T, int P, bool TREE>
 hipError_t launch_combine_p(const void *const *ins, void *out_, uint64_t count, hipStream_t s) {
-    // rocprofv3 trace, 32 MiB blocks (profiles/r01s3_multi_shape_p24.log): P = 8 on
+    // rocprofv3 trace, 32 MiB blocks (profiles/archive/r01s3_multi_shape_p24.log): P = 8 on
     // 1024-thread WGs (0.76-0.80 of peak); P = 4 with 4 vectors per lane 0.78-0.80
     // (2 vectors: 0.72-0.74); P = 2 with 4 vectors per lane 0.74-0.76
     return launch_combine_pu<Op, T, P, TREE, (P >= 8 ? 1 : 4), (P >= 8 ? 1024 : kThreads)>(ins, out_, count, s);

@@ -3,7 +3,7 @@
 // and 16-bit integers, complex PROD, MAXLOC / MINLOC on the 8- and 16-byte
 // pair types, and the x87 long double ops.  Without these the pairs ran the
 // element-granular k_combine_any (0.08-0.54 of the HBM peak at n = 8,
-// profiles/r01s3_multi_sweep.log).
+// profiles/archive/r01s3_multi_sweep.log).
 #include "kernel_table.hpp"
 
 using namespace mpir_hip;

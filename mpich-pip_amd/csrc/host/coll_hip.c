@@ -349,7 +349,7 @@ static int group_exchange(struct MPIX_Hip_comm_s *c, const xfer_t *sends, int ns
  * combine on the same HBM channels at the same moment: 8 x 32 MiB TREE8 fp32
  * ran at 0.689 of the HBM peak with a 32 MiB stride, 0.767 with 32 MiB +
  * 4352 B (4 KiB + 256), 0.717 with + 256 B only (rocprofv3 kernel trace,
- * tools/multi_gap_ab.hip, profiles/r01s3_multi_skew_ab.log).  The skew keeps
+ * tools/multi_gap_ab.hip, profiles/archive/r01s3_multi_skew_ab.log).  The skew keeps
  * the 256 B alignment (fused kernels need the operands equal mod 16). */
 static size_t stage_stride(size_t bytes)
 {

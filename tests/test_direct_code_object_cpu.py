@@ -1,8 +1,8 @@
 """The direct AQL dispatch's code object (lib/libmpir_hip_tiles.hsaco, built
 from csrc/hip/direct_tiles.hip) against what direct_dispatch.hip loads from
 it: for every (op, element class) whose launcher is launch_reduce, the five
-kernels of plan_reduce's launch plan, each with the argument size the host
-writes and no hidden arguments (a bare AQL packet launches them, so a kernel
+kernels of plan_reduce's launch plan in their unchecked and checked forms, each
+taking one 128-byte kernarg slot, and no hidden arguments (a bare AQL packet launches them, so a kernel
 that read gridDim or any other implicit argument would read garbage).  A
 kernel missing or mis-sized here would silently send its calls to the HIP
 launch path (the host skips it), so this pins the contract at build time.
@@ -29,8 +29,9 @@ MATRIX = {
     "LAND": INTS, "LOR": INTS, "BAND": INTS, "BOR": INTS, "BXOR": INTS,
     "LXOR": INTS + REALS + ["F80"], "MAXLOC": PAIRS, "MINLOC": PAIRS,
 }
-# plan kind -> (symbol prefix, kernarg bytes): LeanArgs, TileArgs, ShiftArgs, ElemsArgs
-KINDS = {"mpir_tile_": 32, "mpir_tilex_": 80, "mpir_tiles_": 96, "mpir_elems_": 32, "mpir_elemsu_": 32}
+# plan kind -> kernarg bytes: every kernel takes one 128-byte KargSlot (reduce_kernels.hpp)
+# each plan kind unchecked (mpir_<kind>_) and checked (mpir_c<kind>_)
+KINDS = {f"mpir_{c}{k}_": 128 for c in ("", "c") for k in ("tile", "tilex", "tiles", "elems", "elemsu")}
 
 
 def kernels():
@@ -52,7 +53,7 @@ def kernels():
 def test_every_plan_kernel_present_with_its_argument_size():
     ks = kernels()
     want = {f"{p}{op}_MPIR_HIP_{e}": size for op, es in MATRIX.items() for e in es for p, size in KINDS.items()}
-    assert len(want) == 114 * 5
+    assert len(want) == 114 * 10
     missing = sorted(set(want) - set(ks))
     assert not missing, missing[:10]
     wrong = {k: ks[k][0] for k in want if ks[k][0] != want[k]}

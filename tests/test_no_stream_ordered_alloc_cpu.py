@@ -3,7 +3,7 @@ hipFreeAsync / memory pools).  Round 1's TREE combine fallback did, one
 library stream per host thread, and concurrent MINLOC folds came out
 corrupted (commit e7b5d60): the default pool hands a block freed on one
 stream to another stream while the first stream's kernels still read it
-(tools/mempool_race.hip, profiles/r02/mempool_race.log).  The GPU side of the
+(tools/mempool_race.hip, profiles/archive/r02/mempool_race.log).  The GPU side of the
 regression is test_schedule_fused_gpu.py::test_concurrent_threads_minloc_tree16_regression."""
 import os
 import re

@@ -200,7 +200,7 @@ def test_concurrent_threads_minloc_tree16_regression(mpi, orc, cuda):
     hipMallocAsync / hipFreeAsync, and the default memory pool handed a block
     freed on one stream to another stream while the first stream's kernels
     still read it (tools/mempool_race.hip: 3 of 1200 results corrupted at 4
-    threads, 14 of 2400 at 8; profiles/r02/mempool_race.log).  The product takes
+    threads, 14 of 2400 at 8; profiles/archive/r02/mempool_race.log).  The product takes
     no stream-ordered allocations (tests/test_no_stream_ordered_alloc_cpu.py);
     this checks the concurrent folds stay bit-exact."""
     import threading
