@@ -101,7 +101,8 @@ def main():
     c = lambda k, n: med(vals[k][n])
     row("kernel us (pmc passes)", lambda k: med(durs[k]), "{:14.2f}")
     row("frac of 8 TB/s", lambda k: ALG[k] / (med(durs[k]) * 1e-6) / 8e12)
-    row("EA read bytes / alg read", lambda k: 64 * c(k, "TCC_EA0_RDREQ_sum") /
+    # gfx950 EA read requests are 128 B here (no 32 B ones, 64 B not counted separately)
+    row("EA read reqs x 128 B / alg read", lambda k: 128 * c(k, "TCC_EA0_RDREQ_sum") /
         (ALG[k] - (0 if k == "ro8" else MIB32)))
     row("EA write reqs (64 B) / alg write", lambda k: 64 * c(k, "TCC_EA0_WRREQ_64B_sum") / MIB32)
     row("read reqs 32 B share", lambda k: c(k, "TCC_EA0_RDREQ_32B_sum") / c(k, "TCC_EA0_RDREQ_sum"))
