@@ -122,9 +122,12 @@ void MPIR_Hip_direct_profile(int on);
 uint64_t MPIR_Hip_direct_last_kernel_ns(void);
 
 /* Direct-dispatch diagnostics: the device's state (0 not yet tried, 1 ready,
- * -1..-10 the initialisation step that failed: properties, hsa_init, agents,
+ * 2 ready with every kernarg write made visible by a flush read back before
+ * the doorbell -- the queue's dispatch ids are not its packet indices, as
+ * under a tool that intercepts queues such as rocprofv3 --kernel-trace;
+ * -1..-11 the initialisation step that failed: properties, hsa_init, agents,
  * VRAM pool, HDP register, code-object file, code-object load, kernel
- * symbols, kernarg memory, queue; -20 disabled by
+ * symbols, kernarg memory, queue, error word; -20 disabled by
  * MPIR_CVAR_REDUCE_LOCAL_DISPATCH=hip), and the number of direct calls that
  * first synchronised with work reported pending on the legacy null stream. */
 int MPIR_Hip_direct_state(int dev);

@@ -113,7 +113,8 @@ struct CacheEntry {
 struct DevState {
     std::once_flag once;
     bool ok = false;
-    int state = 0;          // 0 not tried, 1 ready, < 0 the init step that failed (MPIR_Hip_direct_state)
+    int state = 0;          // 0 not tried, 1 ready, 2 ready with flushes read back (readback),
+                            // < 0 the init step that failed (MPIR_Hip_direct_state)
     hsa_agent_t agent{};
     hsa_queue_t *queue = nullptr;               // the calls' queue (no dispatch timestamps)
     hsa_queue_t *pqueue = nullptr;              // the same, timestamps on: calls while profiling is on
@@ -125,6 +126,11 @@ struct DevState {
     CacheEntry cache[kCacheSlots];
     volatile uint32_t *hdp = nullptr;
     uint64_t kobj[2][kPlanKinds][MPIR_HIP_NOPS][MPIR_HIP_NELEMS] = {};   // [checked][plan kind] (kPlanPrefix)
+    uint64_t kprobe = 0;                        // mpir_probe_dispatch_id
+    // a queue's dispatch ids are not its packet indices (an intercepting tool,
+    // probe_ids): every written slot is made visible by a flush read back
+    // before the doorbell, and only unchecked kernels run
+    std::atomic<bool> readback{false};
     std::mutex publish;
     std::atomic<int> queue_error{0};
 };
@@ -281,6 +287,65 @@ const char *elem_name(int e) {
 #undef N
 }
 
+// Write a kernel dispatch packet at `idx` (already reserved: the write index
+// is stored here) and ring the doorbell.
+void publish_packet(hsa_queue_t *q, uint64_t idx, uint64_t ko, void *slot, hsa_signal_t sig, uint32_t wg,
+                    uint32_t groups) {
+    hsa_kernel_dispatch_packet_t *p = (hsa_kernel_dispatch_packet_t *)q->base_address + (idx & (q->size - 1));
+    memset((char *)p + 4, 0, sizeof(*p) - 4);
+    p->workgroup_size_x = (uint16_t)wg;
+    p->workgroup_size_y = 1;
+    p->workgroup_size_z = 1;
+    p->grid_size_x = groups * wg;
+    p->grid_size_y = 1;
+    p->grid_size_z = 1;
+    p->kernel_object = ko;
+    p->kernarg_address = slot;
+    p->completion_signal = sig;
+    const uint16_t header = (HSA_PACKET_TYPE_KERNEL_DISPATCH << HSA_PACKET_HEADER_TYPE) |
+                            (kAcquireScope << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE) |
+                            (kReleaseScope << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE);
+    const uint16_t setup = 1 << HSA_KERNEL_DISPATCH_PACKET_SETUP_DIMENSIONS;
+    hsa_queue_store_write_index_relaxed(q, idx + 1);
+    // the ring may be write-combined VRAM (HSA_ALLOCATE_QUEUE_DEV_MEM): the
+    // packet body must be out of the WC buffers before its header is valid
+    _mm_sfence();
+    __atomic_store_n((uint32_t *)p, (uint32_t)header | ((uint32_t)setup << 16), __ATOMIC_RELEASE);
+}
+
+// Whether queue `q` hands its kernels their packet's index as the dispatch id
+// (the checked kernels' nonce, direct_tiles.hip): two probe dispatches through
+// kernarg slot `slot`, each storing the id it was given.  A tool that
+// intercepts the queue (rocprofv3 --kernel-trace measured: the ids run ahead
+// of the indices) makes them differ; so does a queue the probe cannot run on.
+bool probe_ids(DevState &d, hsa_queue_t *q, char *slot) {
+    if (!d.kprobe) return false;
+    hsa_signal_t s;
+    if (hsa_signal_create(1, 0, nullptr, &s) != HSA_STATUS_SUCCESS) return false;
+    volatile uint64_t *out = reinterpret_cast<volatile uint64_t *>((volatile char *)d.err + 16);
+    bool match = true, done = true;
+    for (int i = 0; i < 2 && match && done; ++i) {
+        KargSlot ks{};
+        ks.w[0] = (uint64_t)(uintptr_t)out;
+        ks.w[6] = (uint64_t)(uintptr_t)d.err;
+        memcpy(slot, &ks, sizeof ks);
+        _mm_sfence();
+        *d.hdp = 1u;
+        (void)*d.hdp;
+        *out = ~0ull;
+        hsa_signal_store_relaxed(s, 1);
+        const uint64_t idx = hsa_queue_load_write_index_relaxed(q);
+        while (idx - hsa_queue_load_read_index_scacquire(q) >= q->size) _mm_pause();
+        publish_packet(q, idx, d.kprobe, slot, s, 64, 1);
+        hsa_signal_store_screlease(q->doorbell_signal, idx);
+        // 2 s: a probe that has not finished by then leaves its signal alive
+        done = hsa_signal_wait_scacquire(s, HSA_SIGNAL_CONDITION_EQ, 0, 2 * g_ts_freq, HSA_WAIT_STATE_ACTIVE) == 0;
+        match = done && *out == idx;
+    }
+    if (done) hsa_signal_destroy(s);
+    return match;
+}
+
 void init_dev(int dev, DevState &d) {
     d.state = -1;
     hipDeviceProp_t prop;
@@ -354,6 +419,20 @@ void init_dev(int dev, DevState &d) {
         }
     }
     if (!found) return;
+    {
+        hsa_executable_symbol_t s;
+        uint32_t kas = 0, lds = 1, priv = 1;
+        if (hsa_executable_get_symbol_by_name(exe, "mpir_probe_dispatch_id.kd", &gpu, &s) == HSA_STATUS_SUCCESS &&
+            hsa_executable_symbol_get_info(s, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_OBJECT, &d.kprobe) == HSA_STATUS_SUCCESS &&
+            hsa_executable_symbol_get_info(s, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_KERNARG_SEGMENT_SIZE, &kas) ==
+                HSA_STATUS_SUCCESS &&
+            hsa_executable_symbol_get_info(s, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_GROUP_SEGMENT_SIZE, &lds) ==
+                HSA_STATUS_SUCCESS &&
+            hsa_executable_symbol_get_info(s, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_PRIVATE_SEGMENT_SIZE, &priv) ==
+                HSA_STATUS_SUCCESS &&
+            (kas != kKargSlotBytes || lds != 0 || priv != 0))
+            d.kprobe = 0;
+    }
     // kernargs in VRAM, host-writable
     d.state = -9;
     void *kp = nullptr;
@@ -384,6 +463,9 @@ void init_dev(int dev, DevState &d) {
     *d.err = 0;
     d.karg = static_cast<char *>(kp);
     d.hdp = hdp.HDP_MEM_FLUSH_CNTL;
+    // the nonce protocol, or flushes read back when the queue's dispatch ids
+    // are not its indices (probe_ids; ring slot 0, rewritten below)
+    if (!probe_ids(d, d.queue, d.karg)) d.readback.store(true);
     // Every slot starts with the error word's address (the same in every later
     // write, so never stale) and nonce 0, below every dispatch id + 1; this
     // once, the flush is read back.
@@ -396,7 +478,7 @@ void init_dev(int dev, DevState &d) {
         (void)*d.hdp;
     }
     d.ok = true;
-    d.state = 1;
+    d.state = d.readback.load() ? 2 : 1;
 }
 
 // The profiled queue is created only when first needed: an idle queue that
@@ -410,6 +492,8 @@ hsa_queue_t *profiled_queue(DevState &d) {
             return;
         // timestamps on from creation (see kAcquireScope's comment above)
         hsa_amd_profiling_set_profiler_enabled(q, 1);
+        // (its ring's first slot: no profiled dispatch exists yet)
+        if (!probe_ids(d, q, d.karg + (size_t)kProfBase * kKargSlotBytes)) d.readback.store(true);
         d.pqueue = q;
     });
     return d.pqueue ? d.pqueue : d.queue;
@@ -483,6 +567,7 @@ int direct_reduce(int dev, int op, int elem, const ReducePlan &p, int *rc) {
     DevState &d = g_dev[dev];
     std::call_once(d.once, [&] { init_dev(dev, d); });
     if (!d.ok || d.queue_error.load(std::memory_order_relaxed)) return 0;
+    const bool rb = d.readback.load(std::memory_order_relaxed);
     const uint64_t ko = d.kobj[0][p.kind][op][elem], ko_checked = d.kobj[1][p.kind][op][elem];
     // the packet's grid_size_x (workgroups x kThreads) is 32 bits
     if (!ko || !ko_checked || p.groups == 0 || p.groups > (uint64_t)UINT32_MAX / kThreads) return 0;
@@ -576,31 +661,19 @@ int direct_reduce(int dev, int op, int elem, const ReducePlan &p, int *rc) {
                 _mm_sfence();
                 g_kernarg_writes.fetch_add(1, std::memory_order_relaxed);
             }
-            ks[7] = idx + 1;
-            ks[15] = idx + 1;
-            _mm_sfence();
-            *d.hdp = 1u;        // HDP flush, not read back (see kRingSlots)
+            if (!rb) {
+                ks[7] = idx + 1;
+                ks[15] = idx + 1;
+                _mm_sfence();
+                *d.hdp = 1u;        // HDP flush, not read back (see kRingSlots)
+            } else {
+                // dispatch ids are not our indices: the slot is visible before
+                // the doorbell (flush read back) and the unchecked kernel runs
+                *d.hdp = 1u;
+                (void)*d.hdp;
+            }
         }
-        hsa_kernel_dispatch_packet_t *p = (hsa_kernel_dispatch_packet_t *)q->base_address + (idx & (q->size - 1));
-        memset((char *)p + 4, 0, sizeof(*p) - 4);
-        p->workgroup_size_x = kThreads;
-        p->workgroup_size_y = 1;
-        p->workgroup_size_z = 1;
-        p->grid_size_x = groups * kThreads;
-        p->grid_size_y = 1;
-        p->grid_size_z = 1;
-        p->kernel_object = checked ? ko_checked : ko;
-        p->kernarg_address = slot;
-        p->completion_signal = sig;
-        const uint16_t header = (HSA_PACKET_TYPE_KERNEL_DISPATCH << HSA_PACKET_HEADER_TYPE) |
-                                (kAcquireScope << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE) |
-                                (kReleaseScope << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE);
-        const uint16_t setup = 1 << HSA_KERNEL_DISPATCH_PACKET_SETUP_DIMENSIONS;
-        hsa_queue_store_write_index_relaxed(q, idx + 1);
-        // the ring may be write-combined VRAM (HSA_ALLOCATE_QUEUE_DEV_MEM): the
-        // packet body must be out of the WC buffers before its header is valid
-        _mm_sfence();
-        __atomic_store_n((uint32_t *)p, (uint32_t)header | ((uint32_t)setup << 16), __ATOMIC_RELEASE);
+        publish_packet(q, idx, checked && !rb ? ko_checked : ko, slot, sig, kThreads, groups);
         if (prof) th1 = sys_ts();
         hsa_signal_store_screlease(q->doorbell_signal, idx);
     }

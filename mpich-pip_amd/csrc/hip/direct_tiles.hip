@@ -108,6 +108,19 @@ __device__ __forceinline__ bool checked_args(KargSlot s, A *a) {
     return true;
 }
 
+// The nonce protocol needs the CP's dispatch id to be the index the host wrote
+// the packet at.  A tool that intercepts the queue (rocprofv3, other
+// HSA_TOOLS_LIB users) re-submits the packets to a hardware queue of its own
+// whose indices differ; the host dispatches this probe at queue creation
+// (direct_dispatch.hip probe_ids) and, when the ids do not match, makes the
+// arguments visible before the doorbell instead (flush read back, unchecked
+// kernels).  Word 0: where lane 0 stores its dispatch id (vector store).
+extern "C" __global__ __launch_bounds__(64) void mpir_probe_dispatch_id(KargSlot ks) {
+    if (threadIdx.x == 0)
+        __hip_atomic_store(reinterpret_cast<uint64_t *>(ks.w[0]), mpir_dispatch_id(), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 template <class A>
 __device__ __forceinline__ bool plain_args(const KargSlot &s, A *a) {
     unpack_args(s, a);

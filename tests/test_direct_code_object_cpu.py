@@ -60,6 +60,14 @@ def test_every_plan_kernel_present_with_its_argument_size():
     assert not wrong, list(wrong.items())[:10]
 
 
+def test_dispatch_id_probe_present():
+    """mpir_probe_dispatch_id: the queue check (direct_dispatch.hip probe_ids)
+    that picks the nonce protocol or read-back flushes; without it the host
+    always takes read-back flushes."""
+    ks = kernels()
+    assert ks.get("mpir_probe_dispatch_id", (0,))[0] == 128
+
+
 def test_no_kernel_reads_a_hidden_argument():
     ks = kernels()
     hidden = sorted(k for k, (_, h, _) in ks.items() if h)

@@ -988,6 +988,8 @@ def test_direct_dispatch_timestamps(mpi, cuda):
     lib = mpi.load()
     assert lib.MPIR_Hip_direct_state(torch.cuda.current_device()) in (0, 1)
     assert mpi.reduce_local(b.data_ptr(), a.data_ptr(), n, mpi.MPI_FLOAT, mpi.MPI_SUM) == 0
+    # 1: the queue's dispatch ids are its packet indices (no intercepting tool),
+    # so the nonce protocol is on
     assert lib.MPIR_Hip_direct_state(torch.cuda.current_device()) == 1
     lib.MPIR_Hip_direct_profile(1)
     try:
