@@ -77,16 +77,20 @@ static_assert(kKargSlotBytes == 128, "one kernarg slot per 128-byte L2 line");
 // cached slot's arguments are rewritten only when no dispatch that uses it
 // is in flight.
 //
-// Every other call writes its slot through the BAR (KargSlot's layout,
-// reduce_kernels.hpp) and dispatches the checked kernel: the argument words
-// that change, an sfence, each half's nonce (the packet's queue index + 1), an
-// sfence, then an HDP flush -- without reading the flush register back, the
-// PCIe round trip that cost every kernarg-cache miss ~1 us before its doorbell
-// (1.7 us from entry to doorbell on a miss against 0.35 us on a hit,
-// profiles/r03/fresh_args_split_before_grid.log).  Correctness does not rest on
-// the flush's timing: the checked kernels (direct_tiles.hip checked_args)
-// re-read a slot whose halves carry a nonce older than their dispatch id + 1,
-// so a workgroup never combines with stale arguments.
+// Every other call dispatches the checked kernel and writes its slot through
+// the BAR (KargSlot's layout, reduce_kernels.hpp) AFTER ringing the doorbell:
+// the argument words that change, an sfence, each half's nonce (the packet's
+// queue index + 1), an sfence, then an HDP flush that is not read back.  The
+// writes overlap the CP's ~4 us from doorbell to dispatch instead of preceding
+// it: round 2 wrote, flushed and read the flush register back first (1.7 us
+// from entry to doorbell on a miss against 0.35 us on a hit,
+// profiles/r03/fresh_args_split_before_grid.log); writing first without the
+// read-back still left a miss 0.5-0.8 us behind a hit, writing after the
+// doorbell 0.1-0.3 us (interleaved, tools/aql/kslot_ab.cpp new_miss /
+// new_miss_late / plain_hit, profiles/r03/kslot_ab_late.log).  Correctness
+// does not rest on the timing: the checked kernels (direct_tiles.hip
+// checked_args) re-read a slot whose halves carry a nonce older than their
+// dispatch id + 1, so a workgroup never combines with stale arguments.
 constexpr uint32_t kRingSlots = 128, kCacheSlots = 128, kProfBase = kRingSlots + kCacheSlots;
 constexpr uint32_t kKargSlots = kProfBase + kRingSlots;
 constexpr uint32_t kQueueSize = 256;
@@ -646,36 +650,43 @@ int direct_reduce(int dev, int op, int elem, const ReducePlan &p, int *rc) {
                 return 0;       // every ring slot in flight: the HIP path takes this call
             }
         }
-        if (checked) {
-            // the argument words that change, then each half's nonce (KargSlot);
-            // the sfences order them on PCIe, so a half showing the nonce holds
-            // its words
-            uint64_t *ks = reinterpret_cast<uint64_t *>(slot);
-            if (write_args) {
-                uint64_t w[12] = {};
-                memcpy(w, ka, kn);
-                for (int i = 0; i < 6; ++i) {
-                    ks[i] = w[i];
-                    ks[8 + i] = w[6 + i];
-                }
-                _mm_sfence();
-                g_kernarg_writes.fetch_add(1, std::memory_order_relaxed);
+        // the argument words that change, then each half's nonce (KargSlot);
+        // the sfences order them on PCIe, so a half showing the nonce holds
+        // its words
+        uint64_t *ks = reinterpret_cast<uint64_t *>(slot);
+        auto write_args_words = [&] {
+            if (!write_args) return;
+            uint64_t w[12] = {};
+            memcpy(w, ka, kn);
+            for (int i = 0; i < 6; ++i) {
+                ks[i] = w[i];
+                ks[8 + i] = w[6 + i];
             }
-            if (!rb) {
-                ks[7] = idx + 1;
-                ks[15] = idx + 1;
-                _mm_sfence();
-                *d.hdp = 1u;        // HDP flush, not read back (see kRingSlots)
-            } else {
-                // dispatch ids are not our indices: the slot is visible before
-                // the doorbell (flush read back) and the unchecked kernel runs
-                *d.hdp = 1u;
-                (void)*d.hdp;
-            }
+            _mm_sfence();
+            g_kernarg_writes.fetch_add(1, std::memory_order_relaxed);
+        };
+        if (checked && rb) {
+            // dispatch ids are not our indices: the slot is visible before the
+            // doorbell (flush read back) and the unchecked kernel runs
+            write_args_words();
+            *d.hdp = 1u;
+            (void)*d.hdp;
         }
         publish_packet(q, idx, checked && !rb ? ko_checked : ko, slot, sig, kThreads, groups);
         if (prof) th1 = sys_ts();
         hsa_signal_store_screlease(q->doorbell_signal, idx);
+        if (checked && !rb) {
+            // After the doorbell: the checked kernel takes its slot only once
+            // the nonce has landed, so the BAR writes and the flush overlap the
+            // CP's ~4 us from doorbell to dispatch instead of preceding it.
+            // (Still under `publish`: a later dispatch that hits this entry
+            // stamps its nonce only after these words.)
+            write_args_words();
+            ks[7] = idx + 1;
+            ks[15] = idx + 1;
+            _mm_sfence();
+            *d.hdp = 1u;        // HDP flush, not read back (see kRingSlots)
+        }
     }
     for (uint64_t it = 1; hsa_signal_load_scacquire(sig) != 0; ++it) {
         if ((it & 0xFFFF) == 0 && d.queue_error.load(std::memory_order_relaxed)) {

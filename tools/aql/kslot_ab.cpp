@@ -10,6 +10,8 @@
 //   new_hit_nf     checked kernel, nonce words stamped, no flush
 //   new_miss       checked kernel, args + nonce + HDP flush (the product's miss)
 //   new_miss_nf    checked kernel, args + nonce, no flush
+//   new_miss_late  new_miss with the args, nonce and flush written after the
+//                  doorbell (the product since round 3's late-write change)
 //   new_hit_rb     checked kernel, nonce + HDP flush + read back
 //   new_nostamp    checked kernel, slot pre-stamped with the largest nonce: no
 //                  host writes (isolates the checked prologue)
@@ -21,7 +23,7 @@
 // Prints per variant the median / p10 / p90 host wall time per call and, from
 // the CP's dispatch timestamps (the queue records them: KSLOT_TS=1, which adds
 // the same ~0.4 us to every variant), the median kernel duration.
-//   HSA_ALLOCATE_QUEUE_DEV_MEM=1 tools/aql/kslot_ab <old.hsaco> <new.hsaco> [calls per variant]
+//   HSA_ALLOCATE_QUEUE_DEV_MEM=1 tools/aql/kslot_ab <old.hsaco | -> <new.hsaco> [calls per variant]
 //   (bash tools/aql/build_kslot.sh)
 #include <hip/hip_runtime.h>
 #include <hsa/hsa.h>
@@ -102,7 +104,9 @@ int main(int argc, char **argv) {
     hsa_amd_hdp_flush_t hdp{};
     HK(hsa_agent_get_info(g_gpu, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_HDP_FLUSH, &hdp));
     volatile uint32_t *flush = hdp.HDP_MEM_FLUSH_CNTL;
-    const uint64_t ko_old = load_kernel(argv[1], "mpir_tile_SUM_MPIR_HIP_F32.kd");
+    // "-" for old.hsaco: no round-2 code object, the old_* variants are skipped
+    const bool have_old = strcmp(argv[1], "-") != 0;
+    const uint64_t ko_old = have_old ? load_kernel(argv[1], "mpir_tile_SUM_MPIR_HIP_F32.kd") : 0;
     const uint64_t ko_new = load_kernel(argv[2], "mpir_ctile_SUM_MPIR_HIP_F32.kd");
     const uint64_t ko_plain = load_kernel(argv[2], "mpir_tile_SUM_MPIR_HIP_F32.kd");
 
@@ -154,14 +158,15 @@ int main(int argc, char **argv) {
     (void)*flush;
 
     enum { OLD_HIT, OLD_MISS, NEW_HIT, NEW_HIT_NF, NEW_MISS, NEW_MISS_NF, NEW_HIT_RB, NEW_NOSTAMP, OLD_HIT_TOUCH,
-           PLAIN_HIT, NV };
+           PLAIN_HIT, NEW_MISS_LATE, NV };
     const char *names[NV] = {"old_hit", "old_miss", "new_hit", "new_hit_nf", "new_miss", "new_miss_nf", "new_hit_rb",
-                             "new_nostamp", "old_hit_touch", "plain_hit"};
+                             "new_nostamp", "old_hit_touch", "plain_hit", "new_miss_late"};
     std::vector<double> t[NV], kt[NV];
     const uint32_t groups = (uint32_t)(bytes / 16384);
     int call = 0;
     for (int it = 0; it < calls + 10; ++it) {
         for (int v = 0; v < NV; ++v, ++call) {
+            if (!have_old && (v == OLD_HIT || v == OLD_MISS || v == OLD_HIT_TOUCH)) continue;
             const int pair = call % 4;
             const double t0 = now();
             const uint64_t idx = hsa_queue_load_write_index_relaxed(q);
@@ -182,6 +187,7 @@ int main(int argc, char **argv) {
             }
             case NEW_NOSTAMP: slot = karg + (12 + pair) * 128; ko = ko_new; break;
             case PLAIN_HIT: slot = karg + (36 + pair) * 128; ko = ko_plain; break;
+            case NEW_MISS_LATE: slot = karg + (40 + (call % 16)) * 128; ko = ko_new; break;   // written below
             case OLD_HIT_TOUCH: {
                 slot = karg + (32 + pair) * 128; ko = ko_old;
                 uint64_t *ks = reinterpret_cast<uint64_t *>(slot);
@@ -212,6 +218,12 @@ int main(int argc, char **argv) {
             _mm_sfence();
             __atomic_store_n((uint32_t *)p, (uint32_t)header | (1u << 16), __ATOMIC_RELEASE);
             hsa_signal_store_screlease(q->doorbell_signal, idx);
+            if (v == NEW_MISS_LATE) {
+                write_new_args(slot, pair); _mm_sfence();
+                uint64_t *ks = reinterpret_cast<uint64_t *>(slot);
+                ks[7] = idx + 1; ks[15] = idx + 1; _mm_sfence();
+                *flush = 1u;
+            }
             while (hsa_signal_load_scacquire(sig) != 0) _mm_pause();
             const double dt = now() - t0;
             if (it >= 10) t[v].push_back(dt * 1e6);
@@ -224,6 +236,7 @@ int main(int argc, char **argv) {
     }
     if (*(volatile uint32_t *)ew) printf("ERROR WORD SET\n");
     for (int v = 0; v < NV; ++v) {
+        if (t[v].empty()) continue;
         std::sort(t[v].begin(), t[v].end());
         const size_t m = t[v].size();
         printf("%-12s median %8.2f us  p10 %8.2f  p90 %8.2f  (%zu calls)", names[v], t[v][m / 2], t[v][m / 10],
