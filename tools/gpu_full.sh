@@ -9,7 +9,7 @@ mkdir -p gpurun_out
 timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu_$TAG.log 2>&1 && \
 timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_$TAG.log 2>&1 && \
 timeout -k 10 300 python bench.py > gpurun_out/bench_$TAG.log 2>&1 && \
-bash tools/profile_r01.sh $TAG
+bash tools/profile_r03.sh $TAG
 rc=$?
 tail -2 gpurun_out/pytest_gpu_$TAG.log; cat gpurun_out/smoke_$TAG.log | grep -v amdgpu.ids; tail -c 1500 gpurun_out/bench_$TAG.log
 exit $rc
