@@ -137,8 +137,15 @@ int MPIR_Hip_direct_state(int dev);
 void MPIR_Hip_direct_last_split(uint64_t out[4]);
 uint64_t MPIR_Hip_direct_busy_skips(void);
 /* Direct calls whose kernel arguments missed the kernarg cache (written into a
- * VRAM slot and made visible with an HDP flush before the doorbell). */
+ * VRAM slot after the doorbell, with an HDP flush; before it under a queue-
+ * intercepting tool). */
 uint64_t MPIR_Hip_direct_kernarg_writes(void);
+/* Test hook: hold every kernarg write that follows a doorbell back by this many
+ * microseconds (0, the default, = none), as if the calling thread were
+ * preempted between ringing and writing.  The dispatched workgroups wait for
+ * the write (tests/test_parity_gpu.py::test_direct_dispatch_preempted_writer);
+ * returns the previous value. */
+uint32_t MPIR_Hip_direct_test_write_delay_us(uint32_t us);
 int MPIR_Hip_thread_contexts(void);
 
 #ifdef __cplusplus

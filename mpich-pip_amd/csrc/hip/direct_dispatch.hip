@@ -52,6 +52,7 @@
 #include <unistd.h>
 
 #include <atomic>
+#include <chrono>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -142,6 +143,7 @@ struct DevState {
 DevState g_dev[kMaxDirectDev];
 std::atomic<uint64_t> g_direct_calls{0};
 std::atomic<uint64_t> g_busy_skips{0};      // calls that first synchronised with a busy null stream
+std::atomic<uint32_t> g_test_write_delay_us{0};   // MPIR_Hip_direct_test_write_delay_us (tests only)
 std::atomic<uint64_t> g_kernarg_writes{0};  // kernarg-cache misses (BAR write + HDP flush)
 // MPIX_Reduce_local_profile: the CP's start / end timestamps of each direct
 // dispatch (hsa_amd_profiling_get_dispatch_time, what rocprofv3 reads), so a
@@ -681,6 +683,10 @@ int direct_reduce(int dev, int op, int elem, const ReducePlan &p, int *rc) {
             // CP's ~4 us from doorbell to dispatch instead of preceding it.
             // (Still under `publish`: a later dispatch that hits this entry
             // stamps its nonce only after these words.)
+            if (const uint32_t dly = g_test_write_delay_us.load(std::memory_order_relaxed)) {
+                const auto t_end = std::chrono::steady_clock::now() + std::chrono::microseconds(dly);
+                while (std::chrono::steady_clock::now() < t_end) _mm_pause();
+            }
             write_args_words();
             ks[7] = idx + 1;
             ks[15] = idx + 1;
@@ -746,5 +752,7 @@ int direct_state(int dev) {
 uint64_t direct_busy_skips() { return g_busy_skips.load(std::memory_order_relaxed); }
 
 uint64_t direct_kernarg_writes() { return g_kernarg_writes.load(std::memory_order_relaxed); }
+
+uint32_t direct_test_write_delay_us(uint32_t us) { return g_test_write_delay_us.exchange(us); }
 
 }  // namespace mpir_hip

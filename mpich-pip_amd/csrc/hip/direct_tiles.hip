@@ -40,10 +40,12 @@ using namespace mpir_hip;
 //                    beat the BAR writes to memory sees an older nonce and
 //                    re-reads past the caches until the write lands.  The CP's
 //                    ~4 us from doorbell to dispatch against the host's
-//                    ~0.5 us of writes makes that rare; if the nonce never
-//                    arrives (10 ms) the workgroup touches nothing and sets
-//                    the error word, and the call fails instead of combining
-//                    stale arguments.
+//                    ~0.5 us of writes makes that rare, and a host thread
+//                    preempted between its doorbell and its writes only makes
+//                    the workgroups wait; if the nonce never arrives (2 s: the
+//                    process was stopped or died) the workgroup touches nothing
+//                    and sets the error word, and the call fails instead of
+//                    combining stale arguments.
 // Measured against round 2's single protocol (tools/aql/kslot_ab.cpp,
 // interleaved call by call, profiles/r03/kslot_ab.log): checking on every call
 // cost hits ~1.2 us (the heavier prologue and the per-call stamp), so hits stay
@@ -91,12 +93,20 @@ __device__ __forceinline__ bool checked_args(KargSlot s, A *a) {
         const uint64_t *g = (const uint64_t *)(uintptr_t)__builtin_amdgcn_kernarg_segment_ptr();
         bool ok = false;
         while (!ok) {
-            __builtin_amdgcn_s_sleep(2);
+            // the writes normally land within a few us of the doorbell; a host
+            // thread preempted between the doorbell and its writes (a CPU-quota
+            // throttle lasts up to the 100 ms period) makes the wait long, and
+            // the workgroups then poll every ~3 us instead of every ~60 ns
+            if (__builtin_amdgcn_s_memrealtime() - t0 < 5000)        // 50 us
+                __builtin_amdgcn_s_sleep(2);
+            else
+                __builtin_amdgcn_s_sleep(127);
             __builtin_amdgcn_s_dcache_inv();
             asm volatile("buffer_inv sc0 sc1" ::: "memory");
             for (int i = 0; i < 16; ++i) s.w[i] = __builtin_nontemporal_load(g + i);
             ok = slot_fresh<A>(s, want);
-            if (!ok && __builtin_amdgcn_s_memrealtime() - t0 > 1000000) {   // 10 ms: never landed
+            // 2 s: never landed (the host process stopped or died after ringing)
+            if (!ok && __builtin_amdgcn_s_memrealtime() - t0 > 200000000) {
                 if (threadIdx.x == 0)
                     __hip_atomic_store(reinterpret_cast<uint32_t *>(s.w[6]), 1u, __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_SYSTEM);

@@ -38,6 +38,7 @@ int direct_state(int dev);
 void direct_last_split(uint64_t out[4]);
 uint64_t direct_busy_skips();
 uint64_t direct_kernarg_writes();
+uint32_t direct_test_write_delay_us(uint32_t us);
 Entry g_table[MPIR_HIP_NOPS][MPIR_HIP_NELEMS];
 multi_fn g_multi[MPIR_HIP_NOPS][MPIR_HIP_NELEMS][2][3];
 
@@ -585,6 +586,7 @@ void MPIR_Hip_direct_last_split(uint64_t out[4]) { direct_last_split(out); }
 uint64_t MPIR_Hip_direct_busy_skips(void) { return direct_busy_skips(); }
 
 uint64_t MPIR_Hip_direct_kernarg_writes(void) { return direct_kernarg_writes(); }
+uint32_t MPIR_Hip_direct_test_write_delay_us(uint32_t us) { return direct_test_write_delay_us(us); }
 
 int MPIR_Hip_thread_contexts(void) {
     std::lock_guard<std::mutex> lk(g_pool_mu);

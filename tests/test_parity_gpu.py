@@ -9,6 +9,7 @@ IEEE round-to-nearest-even operation on both sides (SURVEY.md §8c
 import ctypes
 import json
 import os
+import time
 
 import numpy as np
 import pytest
@@ -924,8 +925,8 @@ def test_direct_dispatch_fresh_args_every_call(mpi, cuda):
     """Every call with new kernel arguments (a window shifted by 256 B each
     time, 1500 calls over 1024 distinct argument sets): each misses the kernarg
     cache, so its arguments are written into a VRAM slot that earlier
-    dispatches read (128 cache slots, each rewritten ~10 times) and made
-    visible by the HDP flush before the doorbell.  A stale read would combine
+    dispatches read (128 cache slots, each rewritten ~10 times), written after
+    the doorbell and awaited by the checked kernel's nonce.  A stale read would combine
     the wrong window: each element's final value counts exactly the calls whose
     window covered it, checked against numpy's replay of the same sequence."""
     torch = cuda
@@ -946,6 +947,57 @@ def test_direct_dispatch_fresh_args_every_call(mpi, cuda):
     assert lib.MPIR_Hip_direct_kernarg_writes() - w0 >= calls - 2 * nbuf
     for j in range(nbuf):
         assert np.array_equal(da[j].cpu().numpy(), want[j]), j
+
+
+def test_direct_dispatch_preempted_writer(mpi, cuda):
+    """A kernarg-cache miss writes its slot after ringing the doorbell; a host
+    thread preempted between the two (a CPU-quota throttle, a page fault) only
+    makes the dispatched workgroups wait for the nonce.  The test hook holds
+    each post-doorbell write back 20 ms -- beyond the first version's 10 ms
+    limit -- for every launch plan the checked kernels serve (lean tile, tile
+    with head / tail, shift, elements): every call completes through the direct
+    path, bit-exact, and the path stays open afterwards."""
+    torch = cuda
+    lib = mpi.load()
+    lib.MPIR_Hip_direct_test_write_delay_us.restype = ctypes.c_uint32
+    lib.MPIR_Hip_direct_test_write_delay_us.argtypes = [ctypes.c_uint32]
+    f = mpi.fast_reduce_local()
+    x = torch.zeros(2, device="cuda")
+    torch.cuda.synchronize()
+    assert f(x.data_ptr(), x.data_ptr() + 4, 1, mpi.MPI_FLOAT, mpi.MPI_SUM) == 0
+    if lib.MPIR_Hip_direct_state(torch.cuda.current_device()) != 1:
+        pytest.skip("direct dispatch not in nonce mode (unavailable or under a queue-intercepting tool)")
+    rng = np.random.default_rng(7)
+    # (count, inbuf byte offset, inoutbuf byte offset): lean tile, head/tail tile, shift, elements
+    shapes = [(1 << 20, 0, 0), ((1 << 20) + 5, 4, 4), ((1 << 20) + 3, 4, 0), (1000, 4, 8)]
+    keep = []                                   # distinct addresses: every call misses the cache
+    prev = lib.MPIR_Hip_direct_test_write_delay_us(20000)
+    try:
+        for rep in range(2):
+            for n, oi, oo in shapes:
+                a = rng.uniform(-1, 1, n).astype(np.float32)
+                b = rng.uniform(-1, 1, n).astype(np.float32)
+                din = torch.zeros(n + 16, dtype=torch.float32, device="cuda")
+                dio = torch.zeros(n + 16, dtype=torch.float32, device="cuda")
+                din[oi // 4: oi // 4 + n] = torch.from_numpy(b).cuda()
+                dio[oo // 4: oo // 4 + n] = torch.from_numpy(a).cuda()
+                keep += [din, dio]
+                torch.cuda.synchronize()
+                d0, w0 = _direct_count(mpi), lib.MPIR_Hip_direct_kernarg_writes()
+                t0 = time.perf_counter()
+                rc = f(din.data_ptr() + oi, dio.data_ptr() + oo, n, mpi.MPI_FLOAT, mpi.MPI_SUM)
+                dt = time.perf_counter() - t0
+                assert rc == 0, mpi.error_string(rc)
+                assert _direct_count(mpi) - d0 == 1 and lib.MPIR_Hip_direct_kernarg_writes() - w0 == 1
+                assert dt >= 0.019, dt            # the call really waited for the held-back write
+                got = dio[oo // 4: oo // 4 + n].cpu().numpy()
+                assert np.array_equal(got.view(np.uint32), (a + b).view(np.uint32)), (n, oi, oo)
+    finally:
+        lib.MPIR_Hip_direct_test_write_delay_us(prev)
+    assert lib.MPIR_Hip_direct_state(torch.cuda.current_device()) == 1
+    d0 = _direct_count(mpi)
+    assert f(din.data_ptr() + oi, dio.data_ptr() + oo, n, mpi.MPI_FLOAT, mpi.MPI_SUM) == 0
+    assert _direct_count(mpi) - d0 == 1
 
 
 def test_direct_dispatch_orders_after_null_stream(mpi, cuda):
