@@ -10,6 +10,8 @@
 #include <stdlib.h>
 #include <string.h>
 #include <sched.h>
+#include <pthread.h>
+#include <sys/syscall.h>
 #include <unistd.h>
 
 #include <algorithm>
@@ -17,6 +19,7 @@
 #include <condition_variable>
 #include <mutex>
 #include <thread>
+#include <vector>
 
 #include "mpir_hip_reduce.h"
 #include "kernel_table.hpp"
@@ -225,15 +228,27 @@ int get_bounce(int dev, size_t bytes, char **out) {
 // with the process, so exit never waits on them.
 class CopyPool {
   public:
-    CopyPool(int nthreads, int copy_parts) : n_(nthreads), copy_n_(std::min(nthreads, copy_parts)), pid_(getpid()) {
-        for (int i = 1; i < n_; ++i) std::thread([this] { work(); }).detach();
+    // `cpus`: the workers may run on these CPUs only (a NUMA node's pool: the
+    // scheduler still balances them over the node); empty: the process's mask
+    CopyPool(int nthreads, int copy_parts, std::vector<int> cpus = {})
+        : n_(nthreads), copy_n_(std::min(nthreads, copy_parts)), pid_(getpid()) {
+        cpu_set_t set;
+        CPU_ZERO(&set);
+        for (int c : cpus) CPU_SET(c, &set);
+        for (int i = 1; i < n_; ++i)
+            std::thread([this, set, pin = !cpus.empty()] {
+                if (pin) (void)pthread_setaffinity_np(pthread_self(), sizeof set, &set);
+                work();
+            }).detach();
     }
     int threads() const { return n_; }
-    // fn(ctx, k) for every k < nparts: part 0 on the calling thread, the rest
-    // on the workers; returns when all are done.  One job at a time: a caller
-    // that finds the workers busy with another thread's job runs its parts
-    // alone rather than waiting, so concurrent callers (other devices, other
-    // host combines) never serialise behind each other.
+    // fn(ctx, k) for every k < nparts, the parts handed out one at a time to
+    // the calling thread and the workers alike, so a slower thread (remote
+    // memory, a throttled or preempted CPU) simply takes fewer; returns when
+    // all are done.  One job at a time: a caller that finds the workers busy
+    // with another thread's job runs its parts alone rather than waiting, so
+    // concurrent callers (other devices, other host combines) never serialise
+    // behind each other.
     void run(size_t nparts, void (*fn)(void *, size_t), void *ctx) {
         std::unique_lock<std::mutex> job(job_mu_, std::defer_lock);
         // a forked child has none of the workers: run alone there
@@ -255,6 +270,13 @@ class CopyPool {
         for (size_t k = 1; k < nparts && k < (size_t)n_; ++k) cv_.notify_one();
         fn(ctx, 0);
         std::unique_lock<std::mutex> lk(mu_);
+        while (next_ < nparts_) {
+            const size_t k = next_++;
+            lk.unlock();
+            fn(ctx, k);
+            lk.lock();
+            --pending_;
+        }
         done_.wait(lk, [this] { return pending_ == 0; });
     }
     // copies split into at most copy_n_ parts: PCIe, not the host's memory,
@@ -334,6 +356,111 @@ CopyPool &copy_pool() {
         return new CopyPool(n, e ? n : 4);
     }();
     return *pool;
+}
+
+// ---- NUMA placement of the host combine ---------------------------------
+// A both-host combine is bound by the host's memory bandwidth, and a thread
+// reading the other socket's memory runs at about half the rate: torch /
+// hipHostMalloc place pinned buffers on the GPU's node while a rank's pageable
+// buffers sit wherever it first touched them, and the floating pool then
+// reads most of one kind remotely (tools/pinned_read_probe.py,
+// profiles/r03/pinned_read_probe.log: the same 256 MiB fp32 SUM at 70-76 GiB/s
+// for pinned operands on node 0 against 100-136 for pageable ones on node 1).
+// When both operands' sampled pages sit on one node, the split runs on a pool
+// confined to that node's CPUs (within the process's affinity mask);
+// MPIR_CVAR_REDUCE_LOCAL_HOST_NUMA=0 keeps the floating pool.
+bool host_numa_enabled() {
+    static const bool on = [] {
+        const char *e = getenv("MPIR_CVAR_REDUCE_LOCAL_HOST_NUMA");
+        return !(e && atoi(e) == 0);
+    }();
+    return on;
+}
+
+int parse_cpulist(const char *path, std::vector<int> &out) {
+    FILE *f = fopen(path, "r");
+    if (!f) return -1;
+    char buf[4096];
+    const bool ok = fgets(buf, sizeof buf, f) != nullptr;
+    fclose(f);
+    if (!ok) return -1;
+    for (char *p = buf; *p && *p != '\n';) {
+        char *end = nullptr;
+        const long a = strtol(p, &end, 10);
+        if (end == p) break;
+        long b = a;
+        p = end;
+        if (*p == '-') {
+            b = strtol(p + 1, &end, 10);
+            p = end;
+        }
+        for (long c = a; c <= b && c < CPU_SETSIZE; ++c) out.push_back((int)c);
+        if (*p == ',') ++p;
+    }
+    return 0;
+}
+
+// per NUMA node: the CPUs of this process's affinity mask on it, the first
+// hardware thread of every core before the second ones
+const std::vector<std::vector<int>> &node_cpus() {
+    static const std::vector<std::vector<int>> nodes = [] {
+        std::vector<std::vector<int>> v;
+        cpu_set_t mask;
+        if (sched_getaffinity(0, sizeof mask, &mask) != 0) return v;
+        for (int node = 0; node < 64; ++node) {
+            char path[96];
+            snprintf(path, sizeof path, "/sys/devices/system/node/node%d/cpulist", node);
+            std::vector<int> all;
+            if (parse_cpulist(path, all) != 0) break;
+            std::vector<int> first, second;
+            for (int c : all) {
+                if (!CPU_ISSET(c, &mask)) continue;
+                snprintf(path, sizeof path, "/sys/devices/system/cpu/cpu%d/topology/thread_siblings_list", c);
+                std::vector<int> sib;
+                (parse_cpulist(path, sib) == 0 && !sib.empty() && sib[0] != c ? second : first).push_back(c);
+            }
+            first.insert(first.end(), second.begin(), second.end());
+            v.push_back(first);
+        }
+        return v;
+    }();
+    return nodes;
+}
+
+// the NUMA node holding the sampled pages of both operands (start, middle and
+// end of each), or -1 (mixed, not yet touched, or unknown)
+int host_node(const void *a, const void *b, size_t bytes) {
+    if (bytes == 0 || node_cpus().size() < 2) return -1;
+    void *pages[6];
+    int status[6];
+    const uintptr_t base[2] = {reinterpret_cast<uintptr_t>(a), reinterpret_cast<uintptr_t>(b)};
+    for (int i = 0; i < 2; ++i) {
+        pages[3 * i] = reinterpret_cast<void *>(base[i] & ~(uintptr_t)4095);
+        pages[3 * i + 1] = reinterpret_cast<void *>((base[i] + bytes / 2) & ~(uintptr_t)4095);
+        pages[3 * i + 2] = reinterpret_cast<void *>((base[i] + bytes - 1) & ~(uintptr_t)4095);
+    }
+    if (syscall(SYS_move_pages, 0, 6, pages, nullptr, status, 0) != 0) return -1;
+    for (int i = 1; i < 6; ++i)
+        if (status[i] != status[0]) return -1;
+    return status[0] >= 0 && status[0] < (int)node_cpus().size() ? status[0] : -1;
+}
+
+// the pool for a both-host combine of `bytes` per operand: pinned to the
+// operands' node when they share one (and it has CPUs of ours), else the
+// floating pool
+CopyPool &combine_pool(const void *a, const void *b, size_t bytes) {
+    static std::mutex mu;
+    static CopyPool *per_node[64] = {};
+    const int node = host_numa_enabled() ? host_node(a, b, bytes) : -1;
+    if (node < 0 || node >= 64 || node_cpus()[(size_t)node].size() < 2) return copy_pool();
+    std::lock_guard<std::mutex> lk(mu);
+    if (!per_node[node]) {
+        const std::vector<int> &cpus = node_cpus()[(size_t)node];
+        const int n = std::min<int>(copy_pool().threads(), (int)cpus.size());
+        // n workers confined to the node's CPUs; the caller helps
+        per_node[node] = new CopyPool(n + 1, 4, cpus);
+    }
+    return *per_node[node];
 }
 
 // LOC_HOST: pageable (or unknown to HIP); LOC_PINNED: page-locked host memory
@@ -695,19 +822,22 @@ int MPIR_Hip_reduce(const void *inbuf, void *inoutbuf, uint64_t count, int op, i
             g_table[op][elem].host(inbuf, inoutbuf, n);
             return MPIR_HIP_OK;
         }
-        // split over the copy pool's threads, parts on 64-byte boundaries
+        // split over a pool's threads (combine_pool: the operands' NUMA node),
+        // parts on 64-byte boundaries
+        CopyPool &pool = combine_pool(inbuf, inoutbuf, (size_t)(count * esz));
         struct H {
             host_fn fn;
             const char *in;
             char *io;
             uint64_t n, part, unit;
         } h{g_table[op][elem].host, static_cast<const char *>(inbuf), static_cast<char *>(inoutbuf), n, 0, unit};
-        // parts of at least 256 KiB: a worker's wake-up costs a few us
-        const uint64_t per = std::max<uint64_t>((n + copy_pool().threads() - 1) / copy_pool().threads(),
+        // four parts per thread, handed out one at a time (a slower thread
+        // takes fewer), of at least 256 KiB: a worker's wake-up costs a few us
+        const uint64_t per = std::max<uint64_t>((n + 4 * (uint64_t)pool.threads() - 1) / (4 * (uint64_t)pool.threads()),
                                                 ((uint64_t)256 << 10) / unit);
         const uint64_t grain = unit >= 64 ? 1 : 64 / unit;
         h.part = (per + grain - 1) / grain * grain;
-        copy_pool().run((size_t)((n + h.part - 1) / h.part), [](void *p, size_t k) {
+        pool.run((size_t)((n + h.part - 1) / h.part), [](void *p, size_t k) {
             const H *h = static_cast<const H *>(p);
             const uint64_t b = k * h->part, e = std::min(h->n, b + h->part);
             h->fn(h->in + b * h->unit, h->io + b * h->unit, e - b);
