@@ -684,6 +684,54 @@ def test_host_path_matrix_vs_oracle(mpi, orc, cuda, op, t):
         run_pair_host(mpi, orc, op, t, n, seed, off)
 
 
+def _node_cpus():
+    nodes, k = [], 0
+    full = os.sched_getaffinity(0)
+    while os.path.exists(f"/sys/devices/system/node/node{k}/cpulist"):
+        cpus = set()
+        for part in open(f"/sys/devices/system/node/node{k}/cpulist").read().strip().split(","):
+            lo, _, hi = part.partition("-")
+            cpus.update(range(int(lo), int(hi or lo) + 1))
+        nodes.append(cpus & full)
+        k += 1
+    return nodes
+
+
+@pytest.mark.parametrize("op,t", [("MPI_SUM", "MPI_FLOAT"), ("MPI_MAX", "MPI_DOUBLE"), ("MPI_BXOR", "MPI_INT"),
+                                  ("MPI_MINLOC", "MPI_FLOAT_INT")])
+def test_host_combine_numa_pools_vs_oracle(mpi, orc, cuda, op, t):
+    """Split host combines (>= 512 KiB per operand) on operands first-touched on
+    each NUMA node of the host (the node pools), on operands straddling two
+    nodes (the floating pool) and with odd part boundaries: bit-exact against
+    the oracle.  On a one-node host every case takes the floating pool."""
+    nodes = [c for c in _node_cpus() if c]
+    full = os.sched_getaffinity(0)
+    rng = np.random.default_rng(2024)
+    n = (3 << 20) // 8 + 5                       # ~3 MiB of 8-byte elements, ragged
+    cases = [(k, None) for k in range(len(nodes))] + ([(0, 1)] if len(nodes) > 1 else [])
+    for first, second in cases:
+        a = T.to_bytes(T.gen(t, n, rng, op))
+        b = T.to_bytes(T.gen(t, n, rng, op))
+        want = a.copy()
+        assert orc.reduce_local(b.copy(), want, n, mpi.DATATYPES[t], mpi.OPS[op]) == 0
+        try:
+            os.sched_setaffinity(0, nodes[first])
+            ha = np.empty_like(a)
+            hb = np.empty_like(b)
+            half = a.size // 2
+            ha[:half] = a[:half]
+            hb[:half] = b[:half]
+            if second is not None:               # the other half on the other node
+                os.sched_setaffinity(0, nodes[second])
+            ha[half:] = a[half:]
+            hb[half:] = b[half:]
+        finally:
+            os.sched_setaffinity(0, full)
+        rc = mpi.reduce_local(hb.ctypes.data, ha.ctypes.data, n, mpi.DATATYPES[t], mpi.OPS[op])
+        assert rc == 0, mpi.error_string(rc)
+        assert same(ha, want, t), explain(ha, want, a, b, ha.size // n)
+
+
 @pytest.mark.parametrize("path", ["host_combine", "mixed_slot"])
 def test_pinned_host_operand_ordered_after_null_stream(mpi, orc, cuda, path):
     """A pinned host operand filled by an async D2H copy on the legacy null
