@@ -12,11 +12,14 @@
 // kernel); with the kernarg cache below and the AQL rings in VRAM
 // (HSA_ALLOCATE_QUEUE_DEV_MEM=1, the library's default: default_rings_in_vram)
 // the gap is 5.2-5.5 us, 4.3 us of it the CP
-// noticing the doorbell (profiles/archive/r02/sync_split_timeline.log, cp_latency.log).  An earlier attempt (round 1) lost because its kernargs sat in host
-// memory (every workgroup read them over PCIe); here they are written through
-// the BAR into VRAM and made visible with an HDP flush (the register ROCr
-// exposes as HSA_AMD_AGENT_INFO_HDP_FLUSH; read back, as HIP does for its
-// device kernargs), before the packet header is published.
+// noticing the doorbell (profiles/archive/r02/sync_split_timeline.log,
+// cp_latency.log).  An earlier attempt (round 1) lost because its kernargs sat
+// in host memory (every workgroup read them over PCIe); here they sit in VRAM:
+// a call that repeats its arguments dispatches a cached slot as it stands, and
+// any other call writes its slot through the BAR after ringing the doorbell,
+// with an HDP flush (the register ROCr exposes as HSA_AMD_AGENT_INFO_HDP_FLUSH)
+// that is not read back, for a checked kernel that waits for the slot's nonce
+// (kRingSlots below).
 //
 // Scope and ordering (the HIP path is used whenever one does not hold):
 //   * synchronous calls on the library's own stream (hip_stream NULL), both
@@ -34,9 +37,12 @@
 // system-scope acquire costs ~7 us of body, aql_sig_nt_sys) and a
 // system-scope release, so the result is visible to every agent -- SDMA
 // copies and the host included -- when the signal fires.  One queue per
-// device (plus its timestamped twin for profiled calls), shared by the threads; a mutex orders packet publication (single
-// producer at a time, doorbell monotonic); no barrier bit, so concurrent
-// threads' kernels overlap; each thread waits on its own signal.
+// device (plus its timestamped twin for profiled calls), shared by the
+// threads; a mutex orders packet publication (single producer at a time,
+// doorbell monotonic); each thread waits on its own signal.  The CP runs a
+// queue's dispatches one after another whatever the barrier bit
+// (tools/aql/concurrent_probe.cpp, profiles/r03/concurrent_probe.log), so
+// concurrent callers on one device take turns, as they would for the HBM.
 // MPIR_CVAR_REDUCE_LOCAL_DISPATCH=hip turns the path off.
 #include <hip/hip_runtime.h>
 #include <hsa/hsa.h>
