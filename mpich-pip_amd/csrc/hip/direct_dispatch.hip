@@ -679,11 +679,21 @@ int direct_reduce(int dev, int op, int elem, const ReducePlan &p, int *rc) {
             write_args_words();
             *d.hdp = 1u;
             (void)*d.hdp;
+        } else if (checked && prof) {
+            // a profiled call (the CP timestamps are the kernel's measured
+            // duration) writes before the doorbell, so that a host thread
+            // preempted between ringing and writing cannot stretch the
+            // interval the readout reports; the nonce still guards the read
+            write_args_words();
+            ks[7] = idx + 1;
+            ks[15] = idx + 1;
+            _mm_sfence();
+            *d.hdp = 1u;
         }
         publish_packet(q, idx, checked && !rb ? ko_checked : ko, slot, sig, kThreads, groups);
         if (prof) th1 = sys_ts();
         hsa_signal_store_screlease(q->doorbell_signal, idx);
-        if (checked && !rb) {
+        if (checked && !rb && !prof) {
             // After the doorbell: the checked kernel takes its slot only once
             // the nonce has landed, so the BAR writes and the flush overlap the
             // CP's ~4 us from doorbell to dispatch instead of preceding it.

@@ -105,6 +105,11 @@ __device__ __forceinline__ bool checked_args(KargSlot s, A *a) {
             asm volatile("buffer_inv sc0 sc1" ::: "memory");
             for (int i = 0; i < 16; ++i) s.w[i] = __builtin_nontemporal_load(g + i);
             ok = slot_fresh<A>(s, want);
+            // another workgroup of this dispatch already gave up: so does this
+            // one at once (every later resident round would wait its own 2 s)
+            if (!ok && __hip_atomic_load(reinterpret_cast<const uint32_t *>(s.w[6]), __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_SYSTEM) != 0u)
+                return false;
             // 2 s: never landed (the host process stopped or died after ringing)
             if (!ok && __builtin_amdgcn_s_memrealtime() - t0 > 200000000) {
                 if (threadIdx.x == 0)
@@ -131,8 +136,18 @@ extern "C" __global__ __launch_bounds__(64) void mpir_probe_dispatch_id(KargSlot
                            __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// unchecked: the plan's argument words as they stand, all loaded up front in
+// one statement (left to itself the compiler sinks the words the tile reads
+// after its early exit into a second, dependent scalar round trip)
 template <class A>
-__device__ __forceinline__ bool plain_args(const KargSlot &s, A *a) {
+__device__ __forceinline__ bool plain_args(KargSlot s, A *a) {
+    if constexpr (kTwoHalves<A>)
+        asm volatile("" : "+s"(s.w[0]), "+s"(s.w[1]), "+s"(s.w[2]), "+s"(s.w[3]), "+s"(s.w[4]), "+s"(s.w[5]),
+                     "+s"(s.w[8]), "+s"(s.w[9]), "+s"(s.w[10]), "+s"(s.w[11]), "+s"(s.w[12]), "+s"(s.w[13]));
+    else if constexpr (sizeof(A) <= 32)
+        asm volatile("" : "+s"(s.w[0]), "+s"(s.w[1]), "+s"(s.w[2]), "+s"(s.w[3]));
+    else
+        asm volatile("" : "+s"(s.w[0]), "+s"(s.w[1]), "+s"(s.w[2]), "+s"(s.w[3]), "+s"(s.w[4]), "+s"(s.w[5]));
     unpack_args(s, a);
     return true;
 }

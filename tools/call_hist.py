@@ -1,0 +1,60 @@
+#!/usr/bin/env python3
+"""Per-call wall time of bench.py's headline loop (synchronous fp32 SUM,
+256 MiB, 4 rotating pairs, compiled binding), to tell a uniform slowdown of a
+box from a few long host-side stalls: percentiles, the slowest calls and their
+positions, and the loop's aggregate rate with and without them.
+  python3 tools/call_hist.py [calls = 3000]
+"""
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "mpich-pip_amd"))
+
+
+def main():
+    calls = int(sys.argv[1]) if len(sys.argv) > 1 else 3000
+    import mpich_pip_amd as m
+    lib = m.load()
+    import numpy as np
+    import torch
+    count = 64 << 20
+    g = torch.Generator(device="cuda").manual_seed(0x5EED)
+    pairs = [((torch.rand(count, device="cuda", generator=g) * 2 - 1), (torch.rand(count, device="cuda", generator=g) * 2 - 1))
+             for _ in range(4)]
+    ptrs = [(a.data_ptr(), b.data_ptr()) for a, b in pairs]
+    torch.cuda.synchronize()
+    f = m.fast_reduce_local()
+    for i in range(50):
+        pin, pio = ptrs[i % 4]
+        f(pin, pio, count, m.MPI_FLOAT, m.MPI_SUM)
+    t = np.empty(calls, np.int64)
+    clk = time.perf_counter_ns
+    t0 = clk()
+    for i in range(calls):
+        pin, pio = ptrs[i % 4]
+        a = clk()
+        f(pin, pio, count, m.MPI_FLOAT, m.MPI_SUM)
+        t[i] = clk() - a
+    total = clk() - t0
+    us = t / 1e3
+    alg = 3 * count * 4
+    q = np.percentile(us, [1, 10, 50, 90, 99, 99.9])
+    print(f"calls {calls}: p1 {q[0]:.2f} p10 {q[1]:.2f} p50 {q[2]:.2f} p90 {q[3]:.2f} p99 {q[4]:.2f} p99.9 {q[5]:.2f} "
+          f"max {us.max():.2f} us; mean {us.mean():.2f} us")
+    slow = np.argsort(us)[::-1][:10]
+    print("slowest:", ", ".join(f"#{k} {us[k]:.1f}" for k in sorted(slow)))
+    for lim in (130.0, 150.0, 300.0, 1000.0):
+        print(f"  calls > {lim:.0f} us: {(us > lim).sum()}  (their excess over the median: {np.clip(us - q[2], 0, None)[us > lim].sum():.0f} us)")
+    print(f"loop rate {alg * calls / (total / 1e9) / 2**30:.1f} GiB/s = {alg * calls / (total / 1e9) / 8e12:.4f} of 8 TB/s; "
+          f"without calls > 150 us {alg * (us <= 150).sum() / (us[us <= 150].sum() / 1e6) / 8e12:.4f}")
+    # the bench's own shape: 20 / 100 consecutive calls, worst and best windows
+    for w in (20, 100):
+        s = np.convolve(us, np.ones(w), "valid")
+        print(f"  windows of {w}: best {alg * w / (s.min() / 1e6) / 8e12:.4f}  median {alg * w / (np.median(s) / 1e6) / 8e12:.4f}  "
+              f"worst {alg * w / (s.max() / 1e6) / 8e12:.4f} of 8 TB/s")
+
+
+if __name__ == "__main__":
+    main()
