@@ -56,5 +56,63 @@ def main():
               f"worst {alg * w / (s.max() / 1e6) / 8e12:.4f} of 8 TB/s")
 
 
-if __name__ == "__main__":
+if __name__ == "__main__" and not os.environ.get("SPLIT_TAIL"):
     main()
+
+
+def split_tail(calls: int = 3000):
+    """The same loop with the library's per-call profiling on (the timestamped
+    twin queue: entry -> doorbell -> CP start -> CP end -> host sees, ns), to
+    see which interval the slow calls lose their time in."""
+    import ctypes
+    import mpich_pip_amd as m
+    lib = m.load()
+    import numpy as np
+    import torch
+    count = 64 << 20
+    g = torch.Generator(device="cuda").manual_seed(0x5EED)
+    pairs = [((torch.rand(count, device="cuda", generator=g) * 2 - 1), (torch.rand(count, device="cuda", generator=g) * 2 - 1))
+             for _ in range(4)]
+    ptrs = [(a.data_ptr(), b.data_ptr()) for a, b in pairs]
+    torch.cuda.synchronize()
+    f = m.fast_reduce_local()
+    lib.MPIR_Hip_direct_profile(1)
+    split = (ctypes.c_uint64 * 4)()
+    rows = np.empty((calls, 5))
+    for i in range(50 + calls):
+        pin, pio = ptrs[i % 4]
+        a = time.perf_counter_ns()
+        f(pin, pio, count, m.MPI_FLOAT, m.MPI_SUM)
+        w = time.perf_counter_ns() - a
+        lib.MPIR_Hip_direct_last_split(split)
+        if i >= 50:
+            rows[i - 50] = (w / 1e3, split[0] / 1e3, split[1] / 1e3, (split[2] - split[1]) / 1e3, (split[3] - split[2]) / 1e3)
+    lib.MPIR_Hip_direct_profile(0)
+    names = ("wall", "entry->doorbell", "entry->CP start", "kernel (CP)", "CP end->host sees")
+    med = np.median(rows, axis=0)
+    slow = rows[rows[:, 0] > np.percentile(rows[:, 0], 90)]
+    print(f"profiled calls {calls}: median / mean of the slowest 10 % / max, us")
+    for k, nm in enumerate(names):
+        print(f"  {nm:18s} {med[k]:8.2f} {slow[:, k].mean():8.2f} {rows[:, k].max():8.2f}")
+    # are the slow kernels clustered (a clock / power state) or scattered?
+    kern = rows[:, 3]
+    thr = med[3] + 4.0
+    slow_i = np.nonzero(kern > thr)[0]
+    runs, cur = [], 0
+    for a, b in zip(slow_i, slow_i[1:]):
+        cur += 1
+        if b != a + 1:
+            runs.append(cur)
+            cur = 0
+    if len(slow_i):
+        runs.append(cur + 1)
+    gaps = np.diff(slow_i)
+    print(f"kernels > median + 4 us: {len(slow_i)} of {calls}; runs of consecutive slow calls: "
+          f"{np.bincount(runs)[1:].tolist() if runs else []} (count of runs of length 1, 2, ...); "
+          f"gap between slow calls: median {np.median(gaps) if len(gaps) else 0:.0f}, "
+          f"histogram {np.histogram(gaps, bins=[1, 2, 3, 5, 9, 17, 33, 65, 10**6])[0].tolist() if len(gaps) else []}")
+    print("first 200 kernel times (us):", " ".join(f"{x:.0f}" for x in kern[:200]))
+
+
+if __name__ == "__main__" and os.environ.get("SPLIT_TAIL"):
+    split_tail(int(sys.argv[1]) if len(sys.argv) > 1 else 3000)
