@@ -55,6 +55,7 @@ Extra fields (rank 0):
 from __future__ import annotations
 
 import argparse
+import ctypes
 import json
 import os
 import sys
@@ -410,6 +411,28 @@ def config2(m, lib, pairs, stream, k: int, w: int):
     if "kernel_us" not in out:
         out.update({"kernel_us": round(ev, 2), "kernel_frac": round(alg / (ev * 1e-6) / HBM_PEAK_BPS, 4),
                     "kernel_timing": "HIP events around each stream launch"})
+    # the same synchronous call with every store nt (MPIR_CVAR_REDUCE_LOCAL_KEEP_MB=0):
+    # the default keeps a result of <= 64 MiB in the Infinity Cache for its next
+    # reader (a schedule's next step), which costs a loop where nothing re-reads
+    lib.MPIR_Hip_set_keep_bytes.restype = ctypes.c_uint64
+    lib.MPIR_Hip_set_keep_bytes.argtypes = [ctypes.c_uint64]
+    prev = lib.MPIR_Hip_set_keep_bytes(0)
+    try:
+        nt = {}
+        ns = direct_kernel_ns(lib, call, k, w)
+        if ns is not None:
+            us = sum(ns) / len(ns) * 1e-3
+            nt.update({"kernel_us": round(us, 2), "kernel_frac": round(alg / (us * 1e-6) / HBM_PEAK_BPS, 4)})
+        for i in range(w):
+            call(i)
+        t0 = time.perf_counter()
+        for i in range(k):
+            call(w + i)
+        dt = time.perf_counter() - t0
+        nt.update({"sync_api_frac": round(alg * k / dt / HBM_PEAK_BPS, 4), "policy": "MPIR_CVAR_REDUCE_LOCAL_KEEP_MB=0"})
+        out["nt_stores"] = nt
+    finally:
+        lib.MPIR_Hip_set_keep_bytes(prev)
     return out
 
 

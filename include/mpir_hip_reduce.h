@@ -104,6 +104,12 @@ int MPIR_Hip_device_count(void);
 uint64_t MPIR_Hip_host_max_bytes(void);
 uint64_t MPIR_Hip_set_host_max_bytes(uint64_t bytes);
 
+/* Results of at most this many bytes are stored into the Infinity Cache (sc1)
+ * for their next reader, larger ones bypass it (nt): MPIR_CVAR_REDUCE_LOCAL_KEEP_MB,
+ * default 64 MiB.  The setter changes it at run time and returns the previous
+ * value (bench.py reports config 2 both ways). */
+uint64_t MPIR_Hip_set_keep_bytes(uint64_t bytes);
+
 /* One operand host memory, the other on a device, at most this many bytes
  * (MPIR_CVAR_REDUCE_LOCAL_MIXED_MAX_KB, default 1 MiB): the host operand is
  * copied into the calling thread's pinned, device-mapped slot and the kernel

@@ -47,16 +47,15 @@ multi_fn g_multi[MPIR_HIP_NOPS][MPIR_HIP_NELEMS][2][3];
 
 // Results of at most this many bytes are stored sc1 (into the Infinity Cache)
 // rather than nt: MPIR_CVAR_REDUCE_LOCAL_KEEP_MB (0 = every store nt), default
-// 64 (reduce_kernels.hpp, kKeepBytes).
-uint64_t keep_bytes() {
-    static const uint64_t v = [] {
-        const char *e = getenv("MPIR_CVAR_REDUCE_LOCAL_KEEP_MB");
-        if (!e) return kKeepBytes;
-        const long mb = atol(e);
-        return (uint64_t)(mb >= 0 && mb <= 4096 ? mb : 64) << 20;
-    }();
-    return v;
-}
+// 64 (reduce_kernels.hpp, kKeepBytes); MPIR_Hip_set_keep_bytes() changes it at
+// run time (an MPI_T-style cvar write).
+std::atomic<uint64_t> g_keep{[] {
+    const char *e = getenv("MPIR_CVAR_REDUCE_LOCAL_KEEP_MB");
+    if (!e) return kKeepBytes;
+    const long mb = atol(e);
+    return (uint64_t)(mb >= 0 && mb <= 4096 ? mb : 64) << 20;
+}()};
+uint64_t keep_bytes() { return g_keep.load(std::memory_order_relaxed); }
 
 uint64_t keep_for(uint64_t vbytes) { return vbytes <= keep_bytes() ? vbytes : 0; }
 }  // namespace mpir_hip
@@ -697,6 +696,8 @@ const char *MPIR_Hip_error_string(void) { return ctx().err; }
 uint64_t MPIR_Hip_host_max_bytes(void) { return host_max_bytes(); }
 
 uint64_t MPIR_Hip_set_host_max_bytes(uint64_t bytes) { return g_host_max.exchange(bytes); }
+
+uint64_t MPIR_Hip_set_keep_bytes(uint64_t bytes) { return mpir_hip::g_keep.exchange(bytes); }
 
 uint64_t MPIR_Hip_mixed_max_bytes(void) { return mixed_max_bytes(); }
 
