@@ -56,7 +56,7 @@ def main():
               f"worst {alg * w / (s.max() / 1e6) / 8e12:.4f} of 8 TB/s")
 
 
-if __name__ == "__main__" and not os.environ.get("SPLIT_TAIL"):
+if __name__ == "__main__" and not os.environ.get("SPLIT_TAIL") and not os.environ.get("COLD"):
     main()
 
 
@@ -116,3 +116,33 @@ def split_tail(calls: int = 3000):
 
 if __name__ == "__main__" and os.environ.get("SPLIT_TAIL"):
     split_tail(int(sys.argv[1]) if len(sys.argv) > 1 else 3000)
+
+
+def cold_start(calls: int = 400):
+    """From process start: per-call wall time of the first calls (no warm-up
+    beyond allocating and filling the pairs, as bench.py does), to see whether
+    the driver's shape (5 warm-up calls, 20 timed) catches a ramp."""
+    import mpich_pip_amd as m
+    lib = m.load()
+    import numpy as np
+    import torch
+    count = 64 << 20
+    g = torch.Generator(device="cuda").manual_seed(0x5EED)
+    pairs = [((torch.rand(count, device="cuda", generator=g) * 2 - 1), (torch.rand(count, device="cuda", generator=g) * 2 - 1))
+             for _ in range(4)]
+    ptrs = [(a.data_ptr(), b.data_ptr()) for a, b in pairs]
+    torch.cuda.synchronize()
+    f = m.fast_reduce_local()
+    us = np.empty(calls)
+    for i in range(calls):
+        pin, pio = ptrs[i % 4]
+        a = time.perf_counter_ns()
+        f(pin, pio, count, m.MPI_FLOAT, m.MPI_SUM)
+        us[i] = (time.perf_counter_ns() - a) / 1e3
+    alg = 3 * count * 4
+    for lo, hi in ((0, 5), (5, 25), (25, 45), (45, 100), (100, 200), (200, calls)):
+        print(f"  calls {lo:4d}-{hi:4d}: mean {us[lo:hi].mean():7.2f} us = {alg / (us[lo:hi].mean() * 1e-6) / 8e12:.4f} of 8 TB/s")
+
+
+if __name__ == "__main__" and os.environ.get("COLD"):
+    cold_start()
