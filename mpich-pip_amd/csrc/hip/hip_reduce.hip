@@ -410,7 +410,8 @@ const std::vector<std::vector<int>> &node_cpus() {
             char path[96];
             snprintf(path, sizeof path, "/sys/devices/system/node/node%d/cpulist", node);
             std::vector<int> all;
-            if (parse_cpulist(path, all) != 0) break;
+            v.emplace_back();
+            if (parse_cpulist(path, all) != 0) continue;     // node ids need not be contiguous
             std::vector<int> first, second;
             for (int c : all) {
                 if (!CPU_ISSET(c, &mask)) continue;
@@ -419,17 +420,27 @@ const std::vector<std::vector<int>> &node_cpus() {
                 (parse_cpulist(path, sib) == 0 && !sib.empty() && sib[0] != c ? second : first).push_back(c);
             }
             first.insert(first.end(), second.begin(), second.end());
-            v.push_back(first);
+            v.back() = first;
         }
         return v;
     }();
     return nodes;
 }
 
+// NUMA nodes with CPUs this process may use
+int usable_nodes() {
+    static const int n = [] {
+        int c = 0;
+        for (const auto &cpus : node_cpus()) c += !cpus.empty();
+        return c;
+    }();
+    return n;
+}
+
 // the NUMA node holding the sampled pages of both operands (start, middle and
 // end of each), or -1 (mixed, not yet touched, or unknown)
 int host_node(const void *a, const void *b, size_t bytes) {
-    if (bytes == 0 || node_cpus().size() < 2) return -1;
+    if (bytes == 0 || usable_nodes() < 2) return -1;
     void *pages[6];
     int status[6];
     const uintptr_t base[2] = {reinterpret_cast<uintptr_t>(a), reinterpret_cast<uintptr_t>(b)};
