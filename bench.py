@@ -197,7 +197,7 @@ def sync_loops(m, lib, reduce_local, ptrs, count, k: int, w: int, sync, barrier,
     cache then holds) and the same loop with fresh arguments on every call: the
     pairs shifted by multiples of 256 B (same count, same alignment, same
     kernel), 1024 distinct argument sets, so every call writes its arguments
-    into a VRAM slot (after ringing the doorbell, for the checked kernel).
+    into a VRAM slot (before ringing the doorbell, for the checked kernel).
     Returns seconds of each and the kernarg writes per timed fresh call."""
     dt_f32, op_sum = m.MPI_FLOAT, m.MPI_SUM
     call_args = [(pin, pio, count, dt_f32, op_sum) for pin, pio in ptrs]

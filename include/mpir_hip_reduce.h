@@ -143,14 +143,15 @@ int MPIR_Hip_direct_state(int dev);
 void MPIR_Hip_direct_last_split(uint64_t out[4]);
 uint64_t MPIR_Hip_direct_busy_skips(void);
 /* Direct calls whose kernel arguments missed the kernarg cache (written into a
- * VRAM slot after the doorbell, with an HDP flush; before it under a queue-
+ * VRAM slot before the doorbell, with an HDP flush; read back under a queue-
  * intercepting tool). */
 uint64_t MPIR_Hip_direct_kernarg_writes(void);
-/* Test hook: hold every kernarg write that follows a doorbell back by this many
- * microseconds (0, the default, = none), as if the calling thread were
- * preempted between ringing and writing.  The dispatched workgroups wait for
- * the write (tests/test_parity_gpu.py::test_direct_dispatch_preempted_writer);
- * returns the previous value. */
+/* Test hook: with us > 0, a checked dispatch's kernarg write moves behind the
+ * doorbell and is held back `us` microseconds, as if it had lost the race to
+ * the CP; the dispatched workgroups wait for it
+ * (tests/test_parity_gpu.py::test_direct_dispatch_preempted_writer,
+ * tests/test_direct_timeout_gpu.py, tools/late_write_probe.py).  0, the
+ * default: the write precedes the doorbell.  Returns the previous value. */
 uint32_t MPIR_Hip_direct_test_write_delay_us(uint32_t us);
 int MPIR_Hip_thread_contexts(void);
 

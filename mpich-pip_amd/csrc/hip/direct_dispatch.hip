@@ -16,9 +16,9 @@
 // cp_latency.log).  An earlier attempt (round 1) lost because its kernargs sat
 // in host memory (every workgroup read them over PCIe); here they sit in VRAM:
 // a call that repeats its arguments dispatches a cached slot as it stands, and
-// any other call writes its slot through the BAR after ringing the doorbell,
+// any other call writes its slot through the BAR before ringing the doorbell,
 // with an HDP flush (the register ROCr exposes as HSA_AMD_AGENT_INFO_HDP_FLUSH)
-// that is not read back, for a checked kernel that waits for the slot's nonce
+// that is not read back, for a checked kernel that verifies the slot's nonce
 // (kRingSlots below).
 //
 // Scope and ordering (the HIP path is used whenever one does not hold):
@@ -85,19 +85,18 @@ static_assert(kKargSlotBytes == 128, "one kernarg slot per 128-byte L2 line");
 // is in flight.
 //
 // Every other call dispatches the checked kernel and writes its slot through
-// the BAR (KargSlot's layout, reduce_kernels.hpp) AFTER ringing the doorbell:
+// the BAR before ringing the doorbell (KargSlot's layout, reduce_kernels.hpp):
 // the argument words that change, an sfence, each half's nonce (the packet's
-// queue index + 1), an sfence, then an HDP flush that is not read back.  The
-// writes overlap the CP's ~4 us from doorbell to dispatch instead of preceding
-// it: round 2 wrote, flushed and read the flush register back first (1.7 us
-// from entry to doorbell on a miss against 0.35 us on a hit,
-// profiles/r03/fresh_args_split_before_grid.log); writing first without the
-// read-back still left a miss 0.5-0.8 us behind a hit, writing after the
-// doorbell 0.1-0.3 us (interleaved, tools/aql/kslot_ab.cpp new_miss /
-// new_miss_late / plain_hit, profiles/r03/kslot_ab_late.log).  Correctness
-// does not rest on the timing: the checked kernels (direct_tiles.hip
-// checked_args) re-read a slot whose halves carry a nonce older than their
-// dispatch id + 1, so a workgroup never combines with stale arguments.
+// queue index + 1), an sfence, then an HDP flush that is not read back.  Round
+// 2 read the flush register back (1.7 us from entry to doorbell on a miss
+// against 0.35 us on a hit, profiles/r03/fresh_args_split_before_grid.log);
+// without the read-back a miss runs 0.5-0.8 us behind a hit
+// (tools/aql/kslot_ab.cpp, profiles/r03/kslot_ab*.log).  Correctness does not
+// rest on the timing: the checked kernels (direct_tiles.hip checked_args)
+// re-read a slot whose halves carry a nonce older than their dispatch id + 1,
+// so a workgroup never combines with stale arguments.  (Writing after the
+// doorbell saves another 0.3-0.6 us but loses badly when the write is late:
+// see direct_reduce.)
 constexpr uint32_t kRingSlots = 128, kCacheSlots = 128, kProfBase = kRingSlots + kCacheSlots;
 constexpr uint32_t kKargSlots = kProfBase + kRingSlots;
 constexpr uint32_t kQueueSize = 256;
@@ -673,17 +672,27 @@ int direct_reduce(int dev, int op, int elem, const ReducePlan &p, int *rc) {
             _mm_sfence();
             g_kernarg_writes.fetch_add(1, std::memory_order_relaxed);
         };
+        // The test hook moves the write behind the doorbell, held back
+        // `late` us: what a write that loses the race to the CP would cost
+        // (tools/late_write_probe.py; tests/test_direct_timeout_gpu.py)
+        const uint32_t late = checked && !rb ? g_test_write_delay_us.load(std::memory_order_relaxed) : 0;
         if (checked && rb) {
             // dispatch ids are not our indices: the slot is visible before the
             // doorbell (flush read back) and the unchecked kernel runs
             write_args_words();
             *d.hdp = 1u;
             (void)*d.hdp;
-        } else if (checked && prof) {
-            // a profiled call (the CP timestamps are the kernel's measured
-            // duration) writes before the doorbell, so that a host thread
-            // preempted between ringing and writing cannot stretch the
-            // interval the readout reports; the nonce still guards the read
+        } else if (checked && !late) {
+            // Before the doorbell: the argument words, then the nonce, then an
+            // HDP flush that is not read back.  The CP's ~4 us from doorbell to
+            // dispatch lands them long before any workgroup reads the slot; the
+            // checked kernel's nonce guards the rare read that still finds an
+            // older line (direct_tiles.hip checked_args).  Written after the
+            // doorbell instead, a miss cost 0.3-0.6 us less per call but a
+            // write that lost the race stalled every first-round workgroup in
+            // L2 invalidations: +57 us for a write 2 us late, +180 us at 4 us
+            // (profiles/r03/late_write_probe.log), and fresh-argument loops
+            // 3-6 % slow on some boxes.
             write_args_words();
             ks[7] = idx + 1;
             ks[15] = idx + 1;
@@ -693,21 +702,14 @@ int direct_reduce(int dev, int op, int elem, const ReducePlan &p, int *rc) {
         publish_packet(q, idx, checked && !rb ? ko_checked : ko, slot, sig, kThreads, groups);
         if (prof) th1 = sys_ts();
         hsa_signal_store_screlease(q->doorbell_signal, idx);
-        if (checked && !rb && !prof) {
-            // After the doorbell: the checked kernel takes its slot only once
-            // the nonce has landed, so the BAR writes and the flush overlap the
-            // CP's ~4 us from doorbell to dispatch instead of preceding it.
-            // (Still under `publish`: a later dispatch that hits this entry
-            // stamps its nonce only after these words.)
-            if (const uint32_t dly = g_test_write_delay_us.load(std::memory_order_relaxed)) {
-                const auto t_end = std::chrono::steady_clock::now() + std::chrono::microseconds(dly);
-                while (std::chrono::steady_clock::now() < t_end) _mm_pause();
-            }
+        if (late) {
+            const auto t_end = std::chrono::steady_clock::now() + std::chrono::microseconds(late);
+            while (std::chrono::steady_clock::now() < t_end) _mm_pause();
             write_args_words();
             ks[7] = idx + 1;
             ks[15] = idx + 1;
             _mm_sfence();
-            *d.hdp = 1u;        // HDP flush, not read back (see kRingSlots)
+            *d.hdp = 1u;
         }
     }
     for (uint64_t it = 1; hsa_signal_load_scacquire(sig) != 0; ++it) {

@@ -29,23 +29,21 @@ using namespace mpir_hip;
 //                    it on a kernarg-cache hit whose slot an earlier, checked
 //                    dispatch has already read back complete: nothing is
 //                    written for the call.
-//   mpir_c<kind>_*   checked.  The host rang the doorbell, then wrote the
-//                    slot for this call through the BAR -- the argument words,
-//                    an sfence, the nonce (the packet's queue index + 1, which
-//                    the CP hands every wave as its dispatch id), an HDP flush
-//                    never read back.  A workgroup accepts its slot when the
-//                    halves holding its arguments carry a nonce >= its dispatch
-//                    id + 1 (a later dispatch of the same arguments may have
-//                    re-stamped the slot meanwhile); one whose kernarg fetch
-//                    beat the BAR writes to memory sees an older nonce and
-//                    re-reads past the caches until the write lands.  The CP's
-//                    ~4 us from doorbell to dispatch against the host's
-//                    ~0.5 us of writes makes that rare, and a host thread
-//                    preempted between its doorbell and its writes only makes
-//                    the workgroups wait; if the nonce never arrives (2 s: the
-//                    process was stopped or died) the workgroup touches nothing
-//                    and sets the error word, and the call fails instead of
-//                    combining stale arguments.
+//   mpir_c<kind>_*   checked.  The host wrote the slot for this call through
+//                    the BAR -- the argument words, an sfence, the nonce (the
+//                    packet's queue index + 1, which the CP hands every wave
+//                    as its dispatch id), an HDP flush never read back -- and
+//                    then rang the doorbell.  A workgroup accepts its slot when
+//                    the halves holding its arguments carry a nonce >= its
+//                    dispatch id + 1 (a later dispatch of the same arguments
+//                    may have re-stamped the slot meanwhile); one that still
+//                    finds an older line (the flush not yet through, a copy an
+//                    earlier dispatch left in its XCD's L2) re-reads past the
+//                    caches until the write shows.  If the nonce never
+//                    arrives (2 s: only a test hook's held-back write, or a
+//                    dead host) the workgroup touches nothing and sets the
+//                    error word, and the call fails instead of combining stale
+//                    arguments.
 // Measured against round 2's single protocol (tools/aql/kslot_ab.cpp,
 // interleaved call by call, profiles/r03/kslot_ab.log): checking on every call
 // cost hits ~1.2 us (the heavier prologue and the per-call stamp), so hits stay

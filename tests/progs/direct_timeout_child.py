@@ -1,5 +1,5 @@
 """Child of tests/test_direct_timeout_gpu.py: a kernarg slot that never lands
-in time.  The test hook holds the post-doorbell kernarg write back 2.2 s, past
+in time.  The test hook moves the kernarg write behind the doorbell, 2.2 s late, past
 the checked kernel's 2 s wait, for a 64 MiB fp32 SUM (4,096 workgroups: two
 resident rounds).  The first round gives up and sets the error word; the second
 round starts after that and must give up at once rather than combine the

@@ -1,8 +1,8 @@
-"""A kernarg slot that never lands: the failure mode of the direct dispatch's
-post-doorbell write (direct_tiles.hip checked_args).  Run in a child process,
+"""A kernarg slot that never lands: the failure mode the checked kernels guard
+against (direct_tiles.hip checked_args).  Run in a child process,
 since a timed-out dispatch closes the direct path for the rest of the process:
-the test hook MPIR_Hip_direct_test_write_delay_us holds the write back 2.2 s,
-past the checked kernel's 2 s wait.  The call must fail with MPI_ERR_OTHER and
+the test hook MPIR_Hip_direct_test_write_delay_us moves the write behind the
+doorbell and holds it back 2.2 s, past the checked kernel's 2 s wait.  The call must fail with MPI_ERR_OTHER and
 leave inoutbuf untouched -- the second resident round of workgroups, started
 after the first gave up, must not combine the arguments that arrive 0.2 s
 later -- and the next call must take the HIP path, bit-exact."""

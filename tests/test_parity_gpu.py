@@ -998,13 +998,13 @@ def test_direct_dispatch_fresh_args_every_call(mpi, cuda):
 
 
 def test_direct_dispatch_preempted_writer(mpi, cuda):
-    """A kernarg-cache miss writes its slot after ringing the doorbell; a host
-    thread preempted between the two (a CPU-quota throttle, a page fault) only
-    makes the dispatched workgroups wait for the nonce.  The test hook holds
-    each post-doorbell write back 20 ms -- beyond the first version's 10 ms
-    limit -- for every launch plan the checked kernels serve (lean tile, tile
-    with head / tail, shift, elements): every call completes through the direct
-    path, bit-exact, and the path stays open afterwards."""
+    """A kernarg-cache miss writes its slot before ringing the doorbell; should
+    the write ever lose the race to the CP (the test hook moves it behind the
+    doorbell and holds it back 20 ms, as a host thread preempted at that point
+    would), the dispatched workgroups wait for the nonce instead of combining
+    stale arguments.  For every launch plan the checked kernels serve (lean
+    tile, tile with head / tail, shift, elements): every call completes
+    through the direct path, bit-exact, and the path stays open afterwards."""
     torch = cuda
     lib = mpi.load()
     lib.MPIR_Hip_direct_test_write_delay_us.restype = ctypes.c_uint32

@@ -239,8 +239,11 @@ int main(int argc, char **argv) {
         if (t[v].empty()) continue;
         std::sort(t[v].begin(), t[v].end());
         const size_t m = t[v].size();
-        printf("%-12s median %8.2f us  p10 %8.2f  p90 %8.2f  (%zu calls)", names[v], t[v][m / 2], t[v][m / 10],
-               t[v][m * 9 / 10], m);
+        double mean = 0;
+        for (double x : t[v]) mean += x;
+        mean /= (double)m;
+        printf("%-12s median %8.2f us  p10 %8.2f  p90 %8.2f  p99 %8.2f  max %8.2f  mean %8.2f  (%zu calls)", names[v],
+               t[v][m / 2], t[v][m / 10], t[v][m * 9 / 10], t[v][m * 99 / 100], t[v][m - 1], mean, m);
         if (!kt[v].empty()) {
             std::sort(kt[v].begin(), kt[v].end());
             printf("  kernel median %8.2f us", kt[v][kt[v].size() / 2]);
