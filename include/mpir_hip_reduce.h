@@ -137,6 +137,12 @@ uint64_t MPIR_Hip_direct_last_kernel_ns(void);
  * MPIR_CVAR_REDUCE_LOCAL_DISPATCH=hip), and the number of direct calls that
  * first synchronised with work reported pending on the legacy null stream. */
 int MPIR_Hip_direct_state(int dev);
+/* Initialise device `dev`'s direct path now -- its HSA queue, the device-only
+ * code object, the kernarg slots, the dispatch-id probe (2-10 ms) -- rather
+ * than inside the first synchronous call on that device; meant for MPI_Init
+ * (Option 1).  Idempotent and thread-safe; returns
+ * MPIR_Hip_direct_state(dev). */
+int MPIR_Hip_direct_prepare(int dev);
 /* With profiling on, the calling thread's last direct call on the system
  * clock, ns from entering the dispatch: doorbell rung, CP start, CP end,
  * completion seen by the host. */

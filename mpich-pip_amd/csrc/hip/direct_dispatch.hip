@@ -761,6 +761,17 @@ void direct_last_split(uint64_t out[4]) {
     for (int i = 0; i < 4; ++i) out[i] = t_last_split[i];
 }
 
+// Initialise device `dev`'s direct path now (HSA queue, the 3.4 MB code object,
+// kernarg slots, the dispatch-id probe: 2-10 ms) instead of in its first call;
+// for MPI_Init-time integration.  Returns direct_state().
+int direct_prepare(int dev) {
+    if (mode() == 0) return -20;
+    if (dev < 0 || dev >= kMaxDirectDev) return -21;
+    DevState &d = g_dev[dev];
+    std::call_once(d.once, [&] { init_dev(dev, d); });
+    return d.state;
+}
+
 int direct_state(int dev) {
     if (mode() == 0) return -20;
     if (dev < 0 || dev >= kMaxDirectDev) return -21;

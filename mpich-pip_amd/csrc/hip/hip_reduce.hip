@@ -38,6 +38,7 @@ uint64_t direct_calls();
 void direct_profile(int on);
 uint64_t direct_last_kernel_ns();
 int direct_state(int dev);
+int direct_prepare(int dev);
 void direct_last_split(uint64_t out[4]);
 uint64_t direct_busy_skips();
 uint64_t direct_kernarg_writes();
@@ -719,6 +720,8 @@ void MPIR_Hip_direct_profile(int on) { direct_profile(on); }
 uint64_t MPIR_Hip_direct_last_kernel_ns(void) { return direct_last_kernel_ns(); }
 
 int MPIR_Hip_direct_state(int dev) { return direct_state(dev); }
+
+int MPIR_Hip_direct_prepare(int dev) { return direct_prepare(dev); }
 
 void MPIR_Hip_direct_last_split(uint64_t out[4]) { direct_last_split(out); }
 
