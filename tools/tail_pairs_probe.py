@@ -63,5 +63,44 @@ def main():
             torch.cuda.empty_cache()
 
 
-if __name__ == "__main__":
+if __name__ == "__main__" and not os.environ.get("MATRIX"):
     main()
+
+
+def matrix(nbuf=8, reps=150):
+    """Median call time for every ordered (inbuf, inoutbuf) pair of `nbuf`
+    separately allocated 256 MiB operands: is a slow pair a property of one
+    buffer or of the two buffers' relative placement?"""
+    import numpy as np
+    import torch
+    import mpich_pip_amd as m
+    m.load()
+    f = m.fast_reduce_local()
+    count = 64 << 20
+    clk = time.perf_counter_ns
+    bufs = [torch.empty(count, device="cuda").uniform_(-1, 1) for _ in range(nbuf)]
+    torch.cuda.synchronize()
+    print("buffers (VA, MiB offset from buffer 0):",
+          " ".join(f"{i}:{(b.data_ptr() - bufs[0].data_ptr()) / 2**20:+.0f}" for i, b in enumerate(bufs)))
+    med = np.zeros((nbuf, nbuf))
+    for rnd in range(2):
+        for i in range(nbuf):
+            for j in range(nbuf):
+                if i == j:
+                    continue
+                pin, pio = bufs[i].data_ptr(), bufs[j].data_ptr()
+                for _ in range(10):
+                    f(pin, pio, count, m.MPI_FLOAT, m.MPI_SUM)
+                t = np.empty(reps)
+                for k in range(reps):
+                    a = clk()
+                    f(pin, pio, count, m.MPI_FLOAT, m.MPI_SUM)
+                    t[k] = (clk() - a) / 1e3
+                med[i, j] = np.median(t)
+        print(f"round {rnd}: median call time (us), row = inbuf, column = inoutbuf")
+        for i in range(nbuf):
+            print(f"  in {i}: " + " ".join("   -   " if i == j else f"{med[i, j]:7.2f}" for j in range(nbuf)), flush=True)
+
+
+if __name__ == "__main__" and os.environ.get("MATRIX"):
+    matrix()
