@@ -56,6 +56,18 @@ __global__ __launch_bounds__(TH) void k_rw(Args a) {
     __builtin_amdgcn_raw_buffer_store_b128(v, ro, off, 0, 2);
 }
 
+// the result written over operand 0's tile (in place, as MPI_Reduce_local
+// writes inoutbuf): P reads + 1 write, the write to rows just read
+template <int P>
+__global__ __launch_bounds__(TH) void k_rwip(Args a) {
+    const uint64_t base = (uint64_t)blockIdx.x * TILE;
+    if (base >= a.vbytes) return;
+    const int off = (int)threadIdx.x * 16;
+    const u32x4 v = fold<P, 0>(a, base, off);
+    __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc((void *)(a.in[0] + base), 0, TILE, 0x00020000);
+    __builtin_amdgcn_raw_buffer_store_b128(v, ro, off, 0, 2);
+}
+
 template <int P, int IL>
 __global__ __launch_bounds__(TH) void k_ro(Args a) {
     const uint64_t base = (uint64_t)blockIdx.x * TILE;
@@ -123,7 +135,15 @@ int main(int argc, char **argv) {
         {"rwk P2 K2", k_rwk<2, 2, 2>, 2, 0, 2},
         {"rwk P1 sc1", k_rwk<1, 1, 16>, 1, 0, 1}, {"rwk P2 sc1", k_rwk<2, 1, 16>, 2, 0, 1},
         {"rwk P4 sc1", k_rwk<4, 1, 16>, 4, 0, 1},
+        {"rwip P1", k_rwip<1>, 1, 0}, {"rwip P2", k_rwip<2>, 2, 0}, {"rwip P4", k_rwip<4>, 4, 0},
+        {"rwip P8", k_rwip<8>, 8, 0},
     };
+    if (getenv("ONLY_RW")) {   // the rw / rwip / ro strided variants only
+        std::vector<Var> keep;
+        for (auto &v : vs)
+            if (!v.IL && v.K == 1 && v.name.find("sc1") == std::string::npos) keep.push_back(v);
+        vs = keep;
+    }
     hipStream_t st;
     CK(hipStreamCreate(&st));
     std::vector<int> order(vs.size());

@@ -23,10 +23,10 @@ for r in csv.DictReader(open(path)):
     d.setdefault(r["Kernel_Name"], []).append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
 rows = []
 for name, v in d.items():
-    m = re.search(r"k_(rwk|rw|ro)<(\d+), (\d+)(?:, (\d+))?>", name)
+    m = re.search(r"k_(rwk|rwip|rw|ro)<(\d+)(?:, (\d+))?(?:, (\d+))?>", name)
     if not m:
         continue
-    kind, p, il = m.group(1), int(m.group(2)), int(m.group(3))
+    kind, p, il = m.group(1), int(m.group(2)), int(m.group(3) or 0)
     if kind == "rwk":
         kind, il = "rw K%d pol%s" % (il, m.group(4)), 0
     v = v[2:] or v
