@@ -973,8 +973,8 @@ def test_direct_dispatch_fresh_args_every_call(mpi, cuda):
     """Every call with new kernel arguments (a window shifted by 256 B each
     time, 1500 calls over 1024 distinct argument sets): each misses the kernarg
     cache, so its arguments are written into a VRAM slot that earlier
-    dispatches read (128 cache slots, each rewritten ~10 times), written after
-    the doorbell and awaited by the checked kernel's nonce.  A stale read would combine
+    dispatches read (128 cache slots, each rewritten ~10 times), written before
+    the doorbell and checked by the kernel's nonce.  A stale read would combine
     the wrong window: each element's final value counts exactly the calls whose
     window covered it, checked against numpy's replay of the same sequence."""
     torch = cuda
@@ -995,6 +995,36 @@ def test_direct_dispatch_fresh_args_every_call(mpi, cuda):
     assert lib.MPIR_Hip_direct_kernarg_writes() - w0 >= calls - 2 * nbuf
     for j in range(nbuf):
         assert np.array_equal(da[j].cpu().numpy(), want[j]), j
+
+
+def test_direct_dispatch_verified_hits_small_grids(mpi, cuda):
+    """A kernarg-cache hit whose slot a checked dispatch has verified runs the
+    UNchecked kernel on the slot as it stands.  With grids of 1-7 workgroups a
+    checked dispatch touches only some XCDs, so an XCD it did not reach could
+    still hold the slot's previous occupant in its L2.  600 operand pairs of
+    1-7 tiles share the 128 cache slots (every slot rewritten many times); each
+    pair is called twice in a row (miss -> checked, then verified hit ->
+    unchecked) and again later.  A stale read would add into the previous
+    occupant's buffers: every buffer must count exactly its own calls."""
+    torch = cuda
+    f = mpi.fast_reduce_local()
+    npairs, rounds = 600, 5
+    sizes = [4096 * (1 + k % 7) for k in range(npairs)]         # 16 KiB tiles: 1-7 workgroups
+    da = [torch.zeros(n, dtype=torch.float32, device="cuda") for n in sizes]
+    db = [torch.ones(n, dtype=torch.float32, device="cuda") for n in sizes]
+    torch.cuda.synchronize()
+    d0 = _direct_count(mpi)
+    rng = np.random.default_rng(7)
+    calls = np.zeros(npairs, np.int64)
+    for _ in range(rounds):
+        for k in rng.permutation(npairs):
+            for _rep in range(2):
+                assert f(db[k].data_ptr(), da[k].data_ptr(), sizes[k], mpi.MPI_FLOAT, mpi.MPI_SUM) == 0
+            calls[k] += 2
+    assert _direct_count(mpi) - d0 == int(calls.sum())
+    for k in range(npairs):
+        got = da[k].cpu().numpy()
+        assert np.all(got == calls[k]), (k, sizes[k], np.unique(got))
 
 
 def test_direct_dispatch_preempted_writer(mpi, cuda):
