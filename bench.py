@@ -92,6 +92,8 @@ def parse():
                     help="TEST ONLY: gloo + a numpy step instead of the GPU call, to exercise the rank "
                          "launch and the max-over-ranks timing on a machine without GPUs")
     ap.add_argument("--no-variants", action="store_true", help="skip sync_variants")
+    ap.add_argument("--only-config5", action="store_true",
+                    help="only the config5_combine block (fp16 two-operand and CHAIN8 kernels), for rocprofv3 passes")
     ap.add_argument("--variant-child", action="store_true", help=argparse.SUPPRESS)
     return ap.parse_args()
 
@@ -141,17 +143,22 @@ def cpu_standin(args) -> None:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
 
-    dt = time_steps(step, args.steps, args.warmup, lambda: None, barrier, max_over_ranks)
+    own = []
+    dt = time_steps(step, args.steps, args.warmup, lambda: None, barrier, max_over_ranks, own)
+    rows = gather_rows([float(rank), own[0]], world, dist, "cpu")
     if rank == 0:
         print(json.dumps({"metric": METRIC, "value": None, "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
                           "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 4),
+                          "per_rank": [{"rank": int(r[0]), "seconds": round(r[1], 6),
+                                        "ms_per_step": round(r[1] / args.steps * 1e3, 4)} for r in rows],
                           "data": "cpu stand-in (test only, not a measurement)"}), flush=True)
     if world > 1:
         dist.destroy_process_group()
 
 
-def time_steps(step, k: int, w: int, sync, barrier, max_over_ranks) -> float:
-    """W untimed steps, then exactly K steps bracketed by barrier + device sync; max over ranks."""
+def time_steps(step, k: int, w: int, sync, barrier, max_over_ranks, own: list | None = None) -> float:
+    """W untimed steps, then exactly K steps bracketed by barrier + device sync; max over ranks.
+    `own`, if given, receives this rank's own seconds (for the per-rank report)."""
     for i in range(w):
         step(i)
     sync()
@@ -163,7 +170,21 @@ def time_steps(step, k: int, w: int, sync, barrier, max_over_ranks) -> float:
     sync()
     t1 = time.perf_counter()
     barrier()
+    if own is not None:
+        own.append(t1 - t0)
     return max_over_ranks(t1 - t0)
+
+
+def gather_rows(row: list, world: int, dist, tensor_device: str) -> list:
+    """Every rank's `row` (floats), in rank order, on every rank (all_gather over
+    the timing group; one row when there is no group)."""
+    if world == 1 or not dist.is_initialized():
+        return [row]
+    import torch
+    t = torch.tensor(row, dtype=torch.float64, device=tensor_device)
+    out = [torch.zeros_like(t) for _ in range(world)]
+    dist.all_gather(out, t)
+    return [x.cpu().tolist() for x in out]
 
 
 def run_collectives_child(rank: int, world: int, local: int, barrier, timeout: float = 180.0):
@@ -191,7 +212,8 @@ def run_collectives_child(rank: int, world: int, local: int, barrier, timeout: f
     return {}
 
 
-def sync_loops(m, lib, reduce_local, ptrs, count, k: int, w: int, sync, barrier, max_over_ranks):
+def sync_loops(m, lib, reduce_local, ptrs, count, k: int, w: int, sync, barrier, max_over_ranks,
+               own: list | None = None):
     """The headline loop (NPAIRS pairs rotated: every call after the first
     NPAIRS repeats its kernel arguments, which the direct dispatch's kernarg
     cache then holds) and the same loop with fresh arguments on every call: the
@@ -212,9 +234,9 @@ def sync_loops(m, lib, reduce_local, ptrs, count, k: int, w: int, sync, barrier,
         rc = reduce_local(*fresh_args[i % len(fresh_args)])
         if rc:
             raise RuntimeError(m.error_string(rc))
-    dt = time_steps(step, k, w, sync, barrier, max_over_ranks)
+    dt = time_steps(step, k, w, sync, barrier, max_over_ranks, own)
     kw0 = lib.MPIR_Hip_direct_kernarg_writes()
-    dtf = time_steps(fstep, k, w, sync, barrier, max_over_ranks)
+    dtf = time_steps(fstep, k, w, sync, barrier, max_over_ranks, own)
     writes = (lib.MPIR_Hip_direct_kernarg_writes() - kw0) / (k + w)
     return dt, dtf, writes, step
 
@@ -436,6 +458,79 @@ def config2(m, lib, pairs, stream, k: int, w: int):
     return out
 
 
+def config5_combine(m, lib, stream, k: int, w: int):
+    """Config 5's combine at one GPU, in its element type (MPIX_C_FLOAT16,
+    mpir_op_util.h:315-319; configure.ac:3122-3131):
+      two_operand  synchronous MPI_Reduce_local fp16 SUM at 256 MiB per operand
+                   (the direct dispatch's mpir_tile_SUM_MPIR_HIP_F16), NPAIRS
+                   pairs rotated, kernel time from the CP's dispatch timestamps;
+      chain8       the fused CHAIN8 fold MPIX_Reduce_local_multi runs for
+                   Reduce_scatter_block's pairwise schedule at 8 ranks
+                   (reduce_scatter_block_intra_pairwise.c:97-134): 8 blocks of
+                   128 MiB, ((x0+x1)+x2)+...+x7 into a 128 MiB output, the blocks
+                   at the collective's skewed staging stride (coll_hip.c
+                   stage_stride: 128 MiB + 4352 B), two sets alternated (2.25 GiB a
+                   cycle, past the 256 MB Infinity Cache); HIP events on the stream.
+    Fractions are algorithmic bytes (3 x 256 MiB; 9 x 128 MiB) over kernel time
+    against 8.0 TB/s; per-launch HBM traffic from the committed PMC summary."""
+    import torch
+    out = {}
+    count = 128 * MIB                           # halves in 256 MiB
+    g = torch.Generator(device="cuda").manual_seed(0xF16)
+    pairs = [((torch.rand(count, device="cuda", generator=g, dtype=torch.float16) * 2 - 1),
+              (torch.rand(count, device="cuda", generator=g, dtype=torch.float16) * 2 - 1)) for _ in range(NPAIRS)]
+    torch.cuda.synchronize()
+    call_args = [(b.data_ptr(), a.data_ptr(), count, m.MPIX_C_FLOAT16, m.MPI_SUM) for a, b in pairs]
+
+    def call(i):
+        rc = lib.MPI_Reduce_local(*call_args[i % NPAIRS])
+        assert rc == 0, m.error_string(rc)
+    alg2 = 3 * count * 2
+    ns = direct_kernel_ns(lib, call, k, w)
+    if ns is not None:
+        us = sum(ns) / len(ns) * 1e-3
+        out["two_operand"] = {"operand_MiB": 256, "kernel": "mpir_tile_SUM_MPIR_HIP_F16 (direct AQL dispatch)",
+                              "kernel_us": round(us, 2), "frac": round(alg2 / (us * 1e-6) / HBM_PEAK_BPS, 4),
+                              "median_us": round(sorted(ns)[len(ns) // 2] * 1e-3, 2),
+                              "timing": "mean of K CP dispatch timestamps"}
+    del pairs, call_args
+    torch.cuda.empty_cache()
+
+    blk = 64 * MIB                              # halves in 128 MiB
+    stride = (blk * 2 + 4352) // 2              # coll_hip.c stage_stride, in halves
+    sets = [torch.empty(8 * stride, device="cuda", dtype=torch.float16) for _ in range(2)]
+    outs = [torch.empty(blk, device="cuda", dtype=torch.float16) for _ in range(2)]
+    for s_ in sets:
+        s_.uniform_(-1, 1, generator=g)
+    torch.cuda.synchronize()
+    ops = [[s_.data_ptr() + 2 * j * stride for j in range(8)] for s_ in sets]
+
+    def launch(i):
+        rc = m.reduce_local_multi(ops[i % 2], outs[i % 2].data_ptr(), blk, m.MPIX_C_FLOAT16, m.MPI_SUM,
+                                  m.MPIX_ORDER_CHAIN, stream.cuda_stream)
+        assert rc == 0, m.error_string(rc)
+    with torch.cuda.stream(stream):
+        us = event_launch_us(launch, k, w, stream)
+    alg8 = 9 * blk * 2
+    out["chain8"] = {"blocks": 8, "block_MiB": 128, "kernel": "k_combine_multi<OpSum, f16, P=8, CHAIN>",
+                     "kernel_us": round(us, 2), "frac": round(alg8 / (us * 1e-6) / HBM_PEAK_BPS, 4),
+                     "timing": "mean of K HIP-event brackets on the launch stream"}
+    del sets, outs
+    torch.cuda.empty_cache()
+    traffic = {}
+    try:
+        traffic = json.load(open(os.path.join(ROOT, "profiles", "pmc_traffic.json"))).get("config5_fp16", {})
+    except (OSError, ValueError):
+        pass
+    for key, alg in (("two_operand", alg2), ("chain8", alg8)):
+        t = traffic.get(key)
+        if key in out and t:
+            out[key].update(traffic=t["hbm_bytes_per_launch"], traffic_over_algorithmic=round(
+                t["hbm_bytes_per_launch"] / alg, 5), rocprof_avg_us=t.get("rocprof_avg_us"),
+                traffic_source="profiles/pmc_traffic.json (config5_fp16)")
+    return out
+
+
 def load_traffic(count_bytes: int):
     """Per-launch HBM bytes of the dominant kernel from the committed PMC summary."""
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
@@ -538,12 +633,14 @@ def main():
     ring_variant = None
     if world == 1 and not args.no_extras and not args.no_variants:
         ring_variant = run_variant_child(args)
+    import mpich_pip_amd as m
+    # the library first, as a program linked against libmpi loads it before
+    # main(): the process is still single-threaded (no numpy / torch yet), so the
+    # library's load-time default puts the AQL rings into VRAM before the HSA
+    # runtime starts (direct_dispatch.hip default_rings_in_vram)
+    lib = m.load()
     import torch
     import torch.distributed as dist
-    import mpich_pip_amd as m
-    # the library first, as a program linked against libmpi loads it before main():
-    # it defaults the AQL rings into VRAM before the HSA runtime starts
-    lib = m.load()
     lib.MPIX_Reduce_local_set_errhandler(m.MPI_ERRORS_RETURN)
     if world != args.gpus:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world} (launched by an external launcher); "
@@ -556,6 +653,10 @@ def main():
     share = os.environ.get("BENCH_TEST_SHARE_GPU") == "1"
     dev = local % torch.cuda.device_count() if share else local
     torch.cuda.set_device(dev)
+    if args.only_config5:
+        print(json.dumps({"config5_combine": config5_combine(m, lib, torch.cuda.Stream(), args.steps, args.warmup)}),
+              flush=True)
+        return
     # BENCH_TEST_PG=1 (test only): the N > 1 plumbing -- RCCL process group,
     # barriers, max over ranks -- at WORLD_SIZE 1, to rehearse it on one GPU
     use_pg = world > 1 or os.environ.get("BENCH_TEST_PG") == "1"
@@ -613,9 +714,16 @@ def main():
         reduce_local, binding = m.fast_reduce_local(), "compiled CPython binding (csrc/py/fastcall.c)"
     except ImportError:     # extension not built: the same C entry point through ctypes
         reduce_local, binding = lib.MPI_Reduce_local, "ctypes"
+    own = []
+    d_before = lib.MPIR_Hip_direct_dispatches()
     dt, dt_fresh, fresh_writes, step = sync_loops(m, lib, reduce_local, ptrs, count, args.steps, args.warmup,
-                                                  sync, barrier, max_over_ranks)
+                                                  sync, barrier, max_over_ranks, own)
+    direct_share = (lib.MPIR_Hip_direct_dispatches() - d_before) / (2 * (args.steps + args.warmup))
     value = alg_bytes * args.steps * world / dt / GIB
+    # each rank's own figures beside the max-over-ranks `value`: a lagging GPU,
+    # or a rank whose calls left the direct path, shows here
+    rows = gather_rows([float(rank), float(dev), own[0], own[1], float(lib.MPIR_Hip_direct_state(dev)),
+                        direct_share], world, dist, "cpu" if pg_backend == "gloo" else "cuda")
 
     def rate(seconds):
         v = alg_bytes * args.steps * world / seconds / GIB
@@ -657,6 +765,13 @@ def main():
                     "frac_of_hbm_peak": round(value / world * GIB / HBM_PEAK_BPS, 4),
                     # the buffer rate count * sizeof(T) / t, for readability
                     "buffer_GiBps": round(value / world / 3, 1)},
+        # every rank's own timed loop (value uses the slowest): seconds, rate,
+        # direct-dispatch state and the share of its calls the direct path took
+        "per_rank": [{"rank": int(r[0]), "device": int(r[1]), "seconds": round(r[2], 6),
+                      "GiBps": round(alg_bytes * args.steps / r[2] / GIB, 1),
+                      "frac_of_hbm_peak": round(alg_bytes * args.steps / r[2] / HBM_PEAK_BPS, 4),
+                      "fresh_args_seconds": round(r[3], 6), "direct_state": int(r[4]),
+                      "direct_share": round(r[5], 4)} for r in rows],
     }
 
     variants = {"fresh_args": dict(rate(dt_fresh), kernarg_writes_per_call=round(fresh_writes, 3),
@@ -733,6 +848,7 @@ def main():
         out["config3_sweep"] = config3_sweep(m, lib, pairs, nbytes, s)
         if nbytes >= 256 * MIB:
             out["config2_64MiB"] = config2(m, lib, pairs, s, args.steps, args.warmup)
+            out["config5_combine"] = config5_combine(m, lib, s, args.steps, args.warmup)
 
         # ---- stream-ordered API, back to back (what the library's schedules drive)
         def sstep(i):

@@ -159,6 +159,12 @@ uint64_t MPIR_Hip_direct_kernarg_writes(void);
  * tests/test_direct_timeout_gpu.py, tools/late_write_probe.py).  0, the
  * default: the write precedes the doorbell.  Returns the previous value. */
 uint32_t MPIR_Hip_direct_test_write_delay_us(uint32_t us);
+/* Test hook: the next probe of a newly created timestamped (profiled) queue
+ * reports that dispatch ids are not packet indices, as under a tool that
+ * intercepts the queue; the first profiled call then switches the device to
+ * read-back flushes (MPIR_Hip_direct_state 2) and must still complete
+ * (tests/test_direct_prepare_gpu.py). */
+void MPIR_Hip_direct_test_fail_probe(void);
 int MPIR_Hip_thread_contexts(void);
 
 #ifdef __cplusplus

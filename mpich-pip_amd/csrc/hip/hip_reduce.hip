@@ -21,6 +21,8 @@
 #include <thread>
 #include <vector>
 
+#include <hsa/hsa.h>
+
 #include "mpir_hip_reduce.h"
 #include "kernel_table.hpp"
 
@@ -43,6 +45,7 @@ void direct_last_split(uint64_t out[4]);
 uint64_t direct_busy_skips();
 uint64_t direct_kernarg_writes();
 uint32_t direct_test_write_delay_us(uint32_t us);
+void direct_test_fail_probe();
 Entry g_table[MPIR_HIP_NOPS][MPIR_HIP_NELEMS];
 multi_fn g_multi[MPIR_HIP_NOPS][MPIR_HIP_NELEMS][2][3];
 
@@ -342,19 +345,33 @@ int usable_cpus() {
     return n;
 }
 
-// Default pool size: the usable CPUs, 4 to 16, for the host combine of large
-// both-host operands, which is memory-bound and scales with threads (256 MiB
-// fp32 SUM on the MI355X host, 16-CPU quota: 131-136 GiB/s on 4 threads,
-// 259-299 on 16; profiles/archive/r02/host_threads_ab.log).  Copies (bounce path,
-// mixed-residency slots) keep to 4 parts, which already outrun a PCIe upload.
-// MPIR_CVAR_REDUCE_LOCAL_STAGE_THREADS sets both.
-CopyPool &copy_pool() {
-    static CopyPool *pool = [] {
-        const char *e = getenv("MPIR_CVAR_REDUCE_LOCAL_STAGE_THREADS");
-        int n = e ? atoi(e) : std::min(16, std::max(4, usable_cpus()));
-        if (n < 1 || n > 64) n = 4;
-        return new CopyPool(n, e ? n : 4);
+// Default pool size: the usable CPUs (affinity mask and cgroup quota), at most
+// 16, for the host combine of large both-host operands, which is memory-bound
+// and scales with threads (256 MiB fp32 SUM on the MI355X host, 16-CPU quota:
+// 131-136 GiB/s on 4 threads, 259-299 on 16;
+// profiles/archive/r02/host_threads_ab.log).  No floor: a rank bound to one
+// CPU (mpiexec --bind-to core) combines on the calling thread alone and the
+// library starts no thread, as MPICH's loop starts none; two CPUs give one
+// worker beside the caller.  Copies (bounce path, mixed-residency slots) keep
+// to at most 4 parts, which already outrun a PCIe upload.
+// MPIR_CVAR_REDUCE_LOCAL_STAGE_THREADS sets both (1 = the caller alone).
+// (pool_threads() sizes a pool without creating one: the floating pool's
+// threads start only when a copy or a combine off the operands' node needs
+// them, never beside a NUMA node's pool that does the work)
+const char *stage_threads_env() {
+    static const char *e = getenv("MPIR_CVAR_REDUCE_LOCAL_STAGE_THREADS");
+    return e;
+}
+int pool_threads() {
+    static const int n = [] {
+        const char *e = stage_threads_env();
+        const int v = e ? atoi(e) : std::min(16, usable_cpus());
+        return v < 1 || v > 64 ? (e ? 4 : 1) : v;
     }();
+    return n;
+}
+CopyPool &copy_pool() {
+    static CopyPool *pool = new CopyPool(pool_threads(), stage_threads_env() ? pool_threads() : 4);
     return *pool;
 }
 
@@ -467,9 +484,10 @@ CopyPool &combine_pool(const void *a, const void *b, size_t bytes) {
     std::lock_guard<std::mutex> lk(mu);
     if (!per_node[node]) {
         const std::vector<int> &cpus = node_cpus()[(size_t)node];
-        const int n = std::min<int>(copy_pool().threads(), (int)cpus.size());
-        // n workers confined to the node's CPUs; the caller helps
-        per_node[node] = new CopyPool(n + 1, 4, cpus);
+        const int n = std::min<int>(pool_threads(), (int)cpus.size());
+        // n - 1 workers confined to the node's CPUs and the caller: no more
+        // threads than the floating pool (the CPUs the process may use)
+        per_node[node] = new CopyPool(n, 4, cpus);
     }
     return *per_node[node];
 }
@@ -554,9 +572,27 @@ uint64_t host_split_bytes() {
     return v;
 }
 
+// Whether this process has started the GPU runtime.  HIP runs on the HSA
+// runtime, and device or pinned memory exists only once it is open, so until
+// then every pointer is pageable host memory and the call needs no HIP query:
+// a CPU-only program linked against libmpi with this drop-in never opens
+// /dev/kfd for its host-buffer reductions, as MPICH's loop (opsum.c:21-76)
+// never does.  hsa_system_get_info answers HSA_STATUS_ERROR_NOT_INITIALIZED
+// without starting anything (ROCr's API table is bound when the library loads;
+// measured: tools/kfd_probe.py), ~2 ns a call; once open, the answer is cached.
+bool gpu_runtime_started() {
+    static std::atomic<bool> up{false};
+    if (up.load(std::memory_order_relaxed)) return true;
+    uint16_t major = 0;
+    if (hsa_system_get_info(HSA_SYSTEM_INFO_VERSION_MAJOR, &major) != HSA_STATUS_SUCCESS) return false;
+    up.store(true, std::memory_order_relaxed);
+    return true;
+}
+
 // Device memory (hipMalloc, managed) is combined in place; host memory
 // (pageable or pinned) takes the host combine, the pinned slot or staging.
 Loc classify(const void *p, int *dev) {
+    if (!gpu_runtime_started()) return LOC_HOST;
     hipPointerAttribute_t at;
     hipError_t e = hipPointerGetAttributes(&at, p);
     if (e != hipSuccess) {
@@ -567,7 +603,9 @@ Loc classify(const void *p, int *dev) {
         *dev = at.device;
         return LOC_DEVICE;
     }
-    return at.type == hipMemoryTypeHost ? LOC_PINNED : LOC_HOST;
+    if (at.type != hipMemoryTypeHost) return LOC_HOST;
+    *dev = at.device;       // the device whose context allocated (registered) it
+    return LOC_PINNED;
 }
 
 // devices visible to this process (0 on a CPU-only rank: host operands are
@@ -593,6 +631,51 @@ int order_after_null_stream() {
     if (hipStreamQuery(nullptr) == hipSuccess) return MPIR_HIP_OK;
     (void)hipGetLastError();
     HIPCHK(hipStreamSynchronize(nullptr));
+    return MPIR_HIP_OK;
+}
+
+// the same for a pinned operand of device `dev`'s context, which the caller may
+// have filled through that device's null stream while another was current
+// (ADVICE r3): that device's null stream, then the caller's device back
+int order_after_null_stream_of(int dev) {
+    int cur = 0;
+    HIPCHK(hipGetDevice(&cur));
+    if (dev < 0 || dev == cur) return order_after_null_stream();
+    HIPCHK(hipSetDevice(dev));
+    const int rc = order_after_null_stream();
+    (void)hipSetDevice(cur);
+    return rc;
+}
+
+// Both operands in host memory: g_table's host loop (the kernels' functors
+// compiled for x86) over n units of `unit` bytes, on the calling thread, or
+// from host_split_bytes() split over a pool's threads (combine_pool: the
+// operands' NUMA node) in parts on 64-byte boundaries.
+int host_combine(int op, int elem, const void *inbuf, void *inoutbuf, uint64_t n, uint64_t unit) {
+    const host_fn fn = g_table[op][elem].host;
+    if (!fn) return MPIR_HIP_ENOKERNEL;
+    if (n * unit < host_split_bytes() || pool_threads() <= 1) {
+        fn(inbuf, inoutbuf, n);
+        return MPIR_HIP_OK;
+    }
+    CopyPool &pool = combine_pool(inbuf, inoutbuf, (size_t)(n * unit));
+    struct H {
+        host_fn fn;
+        const char *in;
+        char *io;
+        uint64_t n, part, unit;
+    } h{fn, static_cast<const char *>(inbuf), static_cast<char *>(inoutbuf), n, 0, unit};
+    // four parts per thread, handed out one at a time (a slower thread takes
+    // fewer), of at least 256 KiB: a worker's wake-up costs a few us
+    const uint64_t per = std::max<uint64_t>((n + 4 * (uint64_t)pool.threads() - 1) / (4 * (uint64_t)pool.threads()),
+                                            ((uint64_t)256 << 10) / unit);
+    const uint64_t grain = unit >= 64 ? 1 : 64 / unit;
+    h.part = (per + grain - 1) / grain * grain;
+    pool.run((size_t)((n + h.part - 1) / h.part), [](void *p, size_t k) {
+        const H *h = static_cast<const H *>(p);
+        const uint64_t b = k * h->part, e = std::min(h->n, b + h->part);
+        h->fn(h->in + b * h->unit, h->io + b * h->unit, e - b);
+    }, &h);
     return MPIR_HIP_OK;
 }
 
@@ -729,6 +812,7 @@ uint64_t MPIR_Hip_direct_busy_skips(void) { return direct_busy_skips(); }
 
 uint64_t MPIR_Hip_direct_kernarg_writes(void) { return direct_kernarg_writes(); }
 uint32_t MPIR_Hip_direct_test_write_delay_us(uint32_t us) { return direct_test_write_delay_us(us); }
+void MPIR_Hip_direct_test_fail_probe(void) { direct_test_fail_probe(); }
 
 int MPIR_Hip_thread_contexts(void) {
     std::lock_guard<std::mutex> lk(g_pool_mu);
@@ -808,14 +892,22 @@ int MPIR_Hip_combine(const void *const *inbufs, int n, void *outbuf, uint64_t co
 
 int MPIR_Hip_reduce(const void *inbuf, void *inoutbuf, uint64_t count, int op, int elem, void *hip_stream,
                     int sync) {
-    ctx().err[0] = 0;
     if (!MPIR_Hip_has_kernel(op, elem)) return MPIR_HIP_ENOKERNEL;
     if (count == 0) return MPIR_HIP_OK;
-    launch_fn fn = g_table[op][elem].fn;
     const size_t esz = g_elem_size[elem];
     // REPLACE is registered as a byte copy: its launcher counts bytes
     const uint64_t unit = (op == MPIR_HIP_OP_REPLACE) ? 1 : esz;
 
+    // ---- no GPU runtime in this process: both operands are pageable host
+    // ---- memory, combined here with no HIP call (the reference's loop,
+    // ---- opsum.c:21-76, touches no device either)
+    if (!gpu_runtime_started() && count * esz <= host_max_bytes()) {
+        if (!sync) return MPIR_HIP_EBUFFER;
+        return host_combine(op, elem, inbuf, inoutbuf, count * esz / unit, unit);
+    }
+
+    ctx().err[0] = 0;
+    launch_fn fn = g_table[op][elem].fn;
     int din = -1, dio = -1;
     const Loc lin = classify(inbuf, &din);
     const Loc lio = classify(inoutbuf, &dio);
@@ -828,36 +920,12 @@ int MPIR_Hip_reduce(const void *inbuf, void *inoutbuf, uint64_t count, int op, i
     // ---- both host-resident: combine on the host (no device needed) ------
     if (lin != LOC_DEVICE && lio != LOC_DEVICE && (count * esz <= host_max_bytes() || device_count() == 0) &&
         g_table[op][elem].host) {
-        if (lin == LOC_PINNED || lio == LOC_PINNED) {
-            const int rc = order_after_null_stream();
-            if (rc != MPIR_HIP_OK) return rc;
-        }
-        const uint64_t n = count * esz / unit;
-        if (count * esz < host_split_bytes() || copy_pool().threads() <= 1) {
-            g_table[op][elem].host(inbuf, inoutbuf, n);
-            return MPIR_HIP_OK;
-        }
-        // split over a pool's threads (combine_pool: the operands' NUMA node),
-        // parts on 64-byte boundaries
-        CopyPool &pool = combine_pool(inbuf, inoutbuf, (size_t)(count * esz));
-        struct H {
-            host_fn fn;
-            const char *in;
-            char *io;
-            uint64_t n, part, unit;
-        } h{g_table[op][elem].host, static_cast<const char *>(inbuf), static_cast<char *>(inoutbuf), n, 0, unit};
-        // four parts per thread, handed out one at a time (a slower thread
-        // takes fewer), of at least 256 KiB: a worker's wake-up costs a few us
-        const uint64_t per = std::max<uint64_t>((n + 4 * (uint64_t)pool.threads() - 1) / (4 * (uint64_t)pool.threads()),
-                                                ((uint64_t)256 << 10) / unit);
-        const uint64_t grain = unit >= 64 ? 1 : 64 / unit;
-        h.part = (per + grain - 1) / grain * grain;
-        pool.run((size_t)((n + h.part - 1) / h.part), [](void *p, size_t k) {
-            const H *h = static_cast<const H *>(p);
-            const uint64_t b = k * h->part, e = std::min(h->n, b + h->part);
-            h->fn(h->in + b * h->unit, h->io + b * h->unit, e - b);
-        }, &h);
-        return MPIR_HIP_OK;
+        int rc = MPIR_HIP_OK;
+        if (lin == LOC_PINNED) rc = order_after_null_stream_of(din);
+        if (rc == MPIR_HIP_OK && lio == LOC_PINNED && !(lin == LOC_PINNED && din == dio))
+            rc = order_after_null_stream_of(dio);
+        if (rc != MPIR_HIP_OK) return rc;
+        return host_combine(op, elem, inbuf, inoutbuf, count * esz / unit, unit);
     }
 
     // ---- small, one operand host memory and the other on a device: the host

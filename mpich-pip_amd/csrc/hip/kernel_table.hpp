@@ -34,6 +34,54 @@ typedef void (*plan_fn)(const void *, void *, uint64_t, ReducePlan *);
 // and REPLACE (a byte copy), which take the HIP launch
 struct Entry { launch_fn fn; any_fn any; host_fn host; plan_fn plan; };
 
+// float / double SUM and PROD on the host: the SSE instruction itself.  The
+// reference's loop `a[i] = a[i] + b[i]` (opsum.c:21-76, gcc -O2) is an
+// addss/addsd (addps/addpd when vectorised) with a[i] -- inout -- as the first
+// source, and x86 applies exactly the NaN rule that x86_result restates for
+// the GPU: the first source if it is a NaN, else the second, quieted; the
+// indefinite for an invalid operation; denormals kept (MXCSR default).  The
+// operand order is pinned with inline asm because the compiler treats
+// addpd/mulpd as commutative.  4 floats / 2 doubles per instruction instead
+// of the functor's per-element NaN checks: 1024 doubles 1.0 -> 0.4 us
+// (tools/host_small_latency.c).  Unaligned operands: movups/movupd.
+template <bool Prod, class T>
+inline bool host_sse(const char *pi, char *po, uint64_t n) {
+#if defined(__x86_64__) && !defined(__HIP_DEVICE_COMPILE__)
+    typedef float v4f __attribute__((vector_size(16), aligned(1)));
+    uint64_t i = 0;
+    constexpr uint64_t per = 16 / sizeof(T);
+    for (; i + per <= n; i += per) {
+        v4f a, b;
+        __builtin_memcpy(&a, po + i * sizeof(T), 16);
+        __builtin_memcpy(&b, pi + i * sizeof(T), 16);
+        if constexpr (sizeof(T) == 4) {
+            if constexpr (Prod) asm("mulps %1, %0" : "+x"(a) : "x"(b));
+            else asm("addps %1, %0" : "+x"(a) : "x"(b));
+        } else {
+            if constexpr (Prod) asm("mulpd %1, %0" : "+x"(a) : "x"(b));
+            else asm("addpd %1, %0" : "+x"(a) : "x"(b));
+        }
+        __builtin_memcpy(po + i * sizeof(T), &a, 16);
+    }
+    for (; i < n; ++i) {
+        T a, b;
+        __builtin_memcpy(&a, po + i * sizeof(T), sizeof(T));
+        __builtin_memcpy(&b, pi + i * sizeof(T), sizeof(T));
+        if constexpr (sizeof(T) == 4) {
+            if constexpr (Prod) asm("mulss %1, %0" : "+x"(a) : "x"(b));
+            else asm("addss %1, %0" : "+x"(a) : "x"(b));
+        } else {
+            if constexpr (Prod) asm("mulsd %1, %0" : "+x"(a) : "x"(b));
+            else asm("addsd %1, %0" : "+x"(a) : "x"(b));
+        }
+        __builtin_memcpy(po + i * sizeof(T), &a, sizeof(T));
+    }
+    return true;
+#else
+    return false;
+#endif
+}
+
 // inout[i] = Op(inout[i], in[i]) on the host, element by element, through the
 // device functors compiled for x86 (unaligned operands: memcpy'd elements)
 template <class Op, class T>
@@ -41,6 +89,8 @@ void host_loop(const void *in, void *io, uint64_t n) {
     Op op;
     const char *pi = static_cast<const char *>(in);
     char *po = static_cast<char *>(io);
+    if constexpr ((__is_same(T, float) || __is_same(T, double)) && (__is_same(Op, OpSum) || __is_same(Op, OpProd)))
+        if (host_sse<__is_same(Op, OpProd), T>(pi, po, n)) return;
     for (uint64_t i = 0; i < n; ++i) {
         T a, b;
         __builtin_memcpy(&a, po + i * sizeof(T), sizeof(T));

@@ -29,3 +29,7 @@ def test_bench_two_ranks_share_one_gpu():
     assert out["n_gpus"] == 2 and out["steps"] == 4 and out["warmup"] == 2
     assert out["data"].startswith("REHEARSAL")
     assert out["value"] > 0 and out["ms_per_step"] > 0
+    # each rank's own loop, its direct-dispatch state and share of direct calls
+    pr = out["per_rank"]
+    assert [r["rank"] for r in pr] == [0, 1], pr
+    assert all(r["seconds"] > 0 and r["direct_state"] in (1, 2) and r["direct_share"] == 1.0 for r in pr), pr

@@ -30,3 +30,17 @@ def test_bench_spawns_two_ranks():
 def test_bench_single_rank_does_not_spawn():
     out = _run(["--gpus", "1", "--steps", "2", "--warmup", "1", "--cpu-standin"])
     assert out["n_gpus"] == 1
+    assert [r["rank"] for r in out["per_rank"]] == [0]
+
+
+def test_bench_eight_ranks_report_per_rank():
+    """at N > 1 the line carries every rank's own timed loop
+    beside the max-over-ranks value, so a lagging GPU (or a rank off the direct
+    path, in the GPU run) is visible.  8 gloo ranks on the CPU."""
+    out = _run(["--gpus", "8", "--steps", "3", "--warmup", "1", "--cpu-standin"], timeout=400)
+    assert out["n_gpus"] == 8
+    pr = out["per_rank"]
+    assert [r["rank"] for r in pr] == list(range(8))
+    assert all(r["seconds"] > 0 for r in pr)
+    # value's time is the slowest rank's
+    assert abs(max(r["ms_per_step"] for r in pr) - out["ms_per_step"]) <= 1e-3 * out["ms_per_step"] + 1e-4
