@@ -101,6 +101,28 @@ constexpr uint32_t kRingSlots = 128, kCacheSlots = 128, kProfBase = kRingSlots +
 constexpr uint32_t kKargSlots = kProfBase + kRingSlots;
 constexpr uint32_t kQueueSize = 256;
 
+// Why a verified slot may be dispatched unchecked on any XCD.  The MI355X's 8
+// XCDs each have their own L2, not coherent with the others
+// (MI355X_MICROARCH.md), and the slot sits in coarse-grained VRAM, which an L2
+// may cache.  A host write (BAR + HDP flush) updates HBM, not a line an XCD's
+// L2 may still hold from an earlier dispatch through the slot.  The packet's
+// agent-scope acquire is HIP's own kernel-to-kernel fence, but the ISA guide
+// and the headers available here do not state that the command processor's
+// acquire invalidates that line in every XCD's L2, so the library does not rely
+// on it: a checked dispatch verifies the slot on every XCD before it counts as
+// verified.  Workgroups are handed to the XCDs round-robin, so a grid of at
+// least 8 reaches all of them; a checked dispatch of a smaller plan is padded
+// to 8 workgroups (the extra ones read and check the slot -- re-reading past the
+// caches if their XCD's line is stale -- and exit, direct_tiles.hip in_grid).
+// After it, every XCD's L2 holds the fresh line or none, and the slot is only
+// rewritten after its entry leaves the cache.  Cost: the seven padding
+// workgroups of a one-workgroup miss (measured in DESIGN.md §Synchronous
+// return); hits pay nothing.
+#ifndef MPIR_DIRECT_MIN_CHECKED_GROUPS
+#define MPIR_DIRECT_MIN_CHECKED_GROUPS 8    // (a build-time override for tools/small_miss_ab.sh only)
+#endif
+constexpr uint32_t kMinCheckedGroups = MPIR_DIRECT_MIN_CHECKED_GROUPS;
+
 // a plan's argument bytes (LeanArgs / TileArgs / ShiftArgs / ElemsArgs,
 // reduce_kernels.hpp; their layouts do not depend on the element type)
 constexpr uint32_t kMaxArgBytes = sizeof(ReducePlan::args);
@@ -735,7 +757,10 @@ int direct_reduce(int dev, int op, int elem, const ReducePlan &p, int *rc) {
             _mm_sfence();
             *d.hdp = 1u;
         }
-        publish_packet(q, idx, checked && !rb ? ko_checked : ko, slot, sig, kThreads, groups);
+        // a checked grid spans every XCD (kMinCheckedGroups): then each XCD's
+        // L2 holds the fresh line, or none, when a later hit runs unchecked
+        publish_packet(q, idx, checked && !rb ? ko_checked : ko, slot, sig, kThreads,
+                       checked && !rb && groups < kMinCheckedGroups ? kMinCheckedGroups : groups);
         if (prof) th1 = sys_ts();
         hsa_signal_store_screlease(q->doorbell_signal, idx);
         if (late) {

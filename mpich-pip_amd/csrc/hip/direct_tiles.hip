@@ -150,7 +150,18 @@ __device__ __forceinline__ bool plain_args(KargSlot s, A *a) {
     return true;
 }
 
-#define MPIR_DIRECT_KIND(PFX, GET, OPN, OP, E, T)                                                         \
+// A checked dispatch of a grid smaller than the chip's 8 XCDs is padded to 8
+// workgroups (direct_dispatch.hip kMinCheckedGroups), so that every XCD's L2
+// has read the slot's fresh line before later cache hits run the unchecked
+// kernel on any XCD.  The padding workgroups check the slot and exit: the tile
+// and shift kernels skip tiles past the region already; the grid-stride
+// element kernels would re-process elements, so they stop a workgroup past the
+// grid the stride was sized for.
+__device__ __forceinline__ bool in_grid(const ElemsArgs &a) {
+    return (uint64_t)blockIdx.x * kThreads < a.stride;
+}
+
+#define MPIR_DIRECT_KIND(PFX, GET, OPN, OP, E, T)                                                       \
     extern "C" __global__ __launch_bounds__(kThreads) void mpir_##PFX##tile_##OPN##_##E(KargSlot ks) {   \
         LeanArgs a;                                                                                       \
         if (GET(ks, &a)) reduce_tile<OP, T>(a.in, a.io, blockIdx.x, a.vbytes, a.keep);                    \
@@ -165,11 +176,11 @@ __device__ __forceinline__ bool plain_args(KargSlot s, A *a) {
     }                                                                                                     \
     extern "C" __global__ __launch_bounds__(kThreads) void mpir_##PFX##elems_##OPN##_##E(KargSlot ks) {  \
         ElemsArgs a;                                                                                      \
-        if (GET(ks, &a)) reduce_elems<OP, T, true>(a.in, a.io, a.n, a.stride);                            \
+        if (GET(ks, &a) && in_grid(a)) reduce_elems<OP, T, true>(a.in, a.io, a.n, a.stride);              \
     }                                                                                                     \
     extern "C" __global__ __launch_bounds__(kThreads) void mpir_##PFX##elemsu_##OPN##_##E(KargSlot ks) { \
         ElemsArgs a;                                                                                      \
-        if (GET(ks, &a)) reduce_elems<OP, T, false>(a.in, a.io, a.n, a.stride);                           \
+        if (GET(ks, &a) && in_grid(a)) reduce_elems<OP, T, false>(a.in, a.io, a.n, a.stride);             \
     }
 
 #define MPIR_DIRECT_TILE(OPN, OP, E, T) MPIR_DIRECT_KIND(, plain_args, OPN, OP, E, T) \
