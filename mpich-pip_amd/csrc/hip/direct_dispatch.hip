@@ -41,7 +41,7 @@
 // threads; a mutex orders packet publication (single producer at a time,
 // doorbell monotonic); each thread waits on its own signal.  The CP runs a
 // queue's dispatches one after another whatever the barrier bit
-// (tools/aql/concurrent_probe.cpp, profiles/r03/concurrent_probe.log), so
+// (tools/aql/concurrent_probe.cpp, profiles/archive/r03/concurrent_probe.log), so
 // concurrent callers on one device take turns, as they would for the HBM.
 // MPIR_CVAR_REDUCE_LOCAL_DISPATCH=hip turns the path off.
 #include <hip/hip_runtime.h>
@@ -89,9 +89,9 @@ static_assert(kKargSlotBytes == 128, "one kernarg slot per 128-byte L2 line");
 // the argument words that change, an sfence, each half's nonce (the packet's
 // queue index + 1), an sfence, then an HDP flush that is not read back.  Round
 // 2 read the flush register back (1.7 us from entry to doorbell on a miss
-// against 0.35 us on a hit, profiles/r03/fresh_args_split_before_grid.log);
+// against 0.35 us on a hit, profiles/archive/r03/fresh_args_split_before_grid.log);
 // without the read-back a miss runs 0.5-0.8 us behind a hit
-// (tools/aql/kslot_ab.cpp, profiles/r03/kslot_ab*.log).  Correctness does not
+// (tools/aql/kslot_ab.cpp, profiles/archive/r03/kslot_ab*.log).  Correctness does not
 // rest on the timing: the checked kernels (direct_tiles.hip checked_args)
 // re-read a slot whose halves carry a nonce older than their dispatch id + 1,
 // so a workgroup never combines with stale arguments.  (Writing after the
@@ -749,7 +749,7 @@ int direct_reduce(int dev, int op, int elem, const ReducePlan &p, int *rc) {
             // doorbell instead, a miss cost 0.3-0.6 us less per call but a
             // write that lost the race stalled every first-round workgroup in
             // L2 invalidations: +57 us for a write 2 us late, +180 us at 4 us
-            // (profiles/r03/late_write_probe.log), and fresh-argument loops
+            // (profiles/archive/r03/late_write_probe.log), and fresh-argument loops
             // 3-6 % slow on some boxes.
             write_args_words();
             ks[7] = idx + 1;

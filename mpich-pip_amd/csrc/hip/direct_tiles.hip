@@ -45,7 +45,7 @@ using namespace mpir_hip;
 //                    error word, and the call fails instead of combining stale
 //                    arguments.
 // Measured against round 2's single protocol (tools/aql/kslot_ab.cpp,
-// interleaved call by call, profiles/r03/kslot_ab.log): checking on every call
+// interleaved call by call, profiles/archive/r03/kslot_ab.log): checking on every call
 // cost hits ~1.2 us (the heavier prologue and the per-call stamp), so hits stay
 // unchecked.
 

@@ -381,7 +381,7 @@ CopyPool &copy_pool() {
 // hipHostMalloc place pinned buffers on the GPU's node while a rank's pageable
 // buffers sit wherever it first touched them, and the floating pool then
 // reads most of one kind remotely (tools/pinned_read_probe.py,
-// profiles/r03/pinned_read_probe.log: the same 256 MiB fp32 SUM at 70-76 GiB/s
+// profiles/archive/r03/pinned_read_probe.log: the same 256 MiB fp32 SUM at 70-76 GiB/s
 // for pinned operands on node 0 against 100-136 for pageable ones on node 1).
 // When both operands' sampled pages sit on one node, the split runs on a pool
 // confined to that node's CPUs (within the process's affinity mask);

@@ -1,4 +1,4 @@
-"""The committed bench line (profiles/r03_bench.log, measured on MI355X) against
+"""The committed bench line (profiles/archive/r03/r03_bench.log, measured on MI355X) against
 the driver's contract and against itself: BASELINE.json's metric, the
 required keys, value = algorithmic bytes x N / time, roofline.frac =
 achieved / peak with achieved = 805,306,368 B / mean launch time, and the
@@ -10,7 +10,7 @@ import os
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LINE = os.path.join(ROOT, "profiles", "r03_bench.log")
+LINE = os.path.join(ROOT, "profiles", "archive", "r03", "r03_bench.log")
 GIB = float(1 << 30)
 
 
@@ -62,7 +62,7 @@ def test_roofline_is_self_consistent(line):
 
 def test_live_kernel_time_agrees_with_rocprof(line):
     """bench.py times the kernel the synchronous call runs; rocprofv3's
-    --kernel-trace --stats average for that kernel (profiles/r03_kernel_stats.csv,
+    --kernel-trace --stats average for that kernel (profiles/archive/r03/r03_kernel_stats.csv,
     summarised in pmc_traffic.json) must agree with it."""
     r = line["roofline"]
     with open(os.path.join(ROOT, "profiles", "pmc_traffic.json")) as f:
