@@ -21,7 +21,8 @@ MIB = 1 << 20
 KERNELS = {
     # key: (name substring(s), algorithmic bytes per launch)
     "two_operand": (("mpir_tile_SUM_MPIR_HIP_F16",), 3 * 256 * MIB),
-    "chain8": (("k_combine_multi", "_Float16, 8, false"), 9 * 128 * MIB),
+    # k_combine_multi<OpSum, _Float16, P = 8, TREE = false (CHAIN), ...>, mangled
+    "chain8": (("k_combine_multi", "OpSumEDF16_Li8ELb0"), 9 * 128 * MIB),
 }
 
 
