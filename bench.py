@@ -699,6 +699,12 @@ def main():
     nbytes = args.mib * MIB
     count = nbytes // 4
     alg_bytes = 3 * nbytes
+    # MPI_Init's share of the library's setup, before the application's data
+    # exists (a program calls MPI_Init, builds its buffers, then reduces): the
+    # direct path's HSA queue, code object and dispatch-id probe
+    # (MPIR_Hip_direct_prepare) rather than inside the
+    # first warm-up call
+    lib.MPIR_Hip_direct_prepare(dev)
     g = torch.Generator(device="cuda").manual_seed(0x5EED + rank)
     # NPAIRS resident pairs, rotated, so no step finds its operands in the
     # 256 MB Infinity Cache (>= 3 pairs)
