@@ -1,0 +1,105 @@
+"""BASELINE configs 2, 4 and 5 at their full sizes on one GPU, against the
+oracle (config 2 at full size was a property check, and
+configs 4 / 5 ran only at size 1 without a second GPU).
+
+  * config 2: MPI_Reduce_local fp32 SUM, 64 MiB per operand -- aligned (the
+    lean tile kernel), ragged (tile + head / tail) and with inbuf 4 B off
+    inoutbuf's alignment (the shift kernel), random operands with the edge
+    values of tests/_types.py, bit-exact against oracle_reduce_local;
+  * config 4's combine: the fused TREE8 fold MPIX_Reduce_local_multi runs for
+    MPI_Allreduce fp32 256 MiB at 8 ranks (one 32 MiB block per owner,
+    reduce_intra_reduce_scatter_gather.c:186-249: ((y0+y1)+(y2+y3))+
+    ((y4+y5)+(y6+y7))), operands at the collective's skewed staging stride;
+  * config 5's combine: the fused CHAIN8 fp16 fold of MPI_Reduce_scatter_block
+    (1 GiB sendbuf, 8 ranks: 8 blocks of 128 MiB,
+    reduce_scatter_block_intra_pairwise.c:97-134: (((x0+x1)+x2)+...)+x7).
+The folds' expected bytes are the oracle's step-by-step MPIR_Reduce_local calls
+in the schedule's association (oracle/op_oracle.c, gcc -O2).  What these do not
+cover is the xGMI transport at 8 ranks (tests/test_coll_rccl_gpu.py, N > 1).
+"""
+import numpy as np
+import pytest
+
+import _types as T
+
+pytestmark = pytest.mark.gpu
+
+MIB = 1 << 20
+
+
+def _dev(torch, arr, slack=0):
+    t = torch.zeros(arr.nbytes + slack, dtype=torch.uint8, device="cuda")
+    t[:arr.nbytes] = torch.from_numpy(arr.view(np.uint8))
+    return t
+
+
+@pytest.mark.parametrize("extra,off", [(0, 0), (3, 0), (1, 4)], ids=["aligned", "ragged", "inbuf+4B"])
+def test_config2_64mib_vs_oracle(mpi, orc, cuda, extra, off):
+    torch = cuda
+    n = (64 * MIB) // 4 + extra
+    rng = np.random.default_rng(64 + extra + off)
+    a = T.gen("MPI_FLOAT", n, rng, "MPI_SUM").view(np.float32)
+    b = T.gen("MPI_FLOAT", n, rng, "MPI_SUM").view(np.float32)
+    want = a.copy()
+    assert orc.reduce_local(b.copy(), want, n, mpi.MPI_FLOAT, mpi.MPI_SUM) == 0
+    tio = _dev(torch, a)
+    tin = torch.zeros(b.nbytes + 64, dtype=torch.uint8, device="cuda")
+    tin[off:off + b.nbytes] = torch.from_numpy(b.view(np.uint8))
+    torch.cuda.synchronize()
+    assert mpi.reduce_local(tin.data_ptr() + off, tio.data_ptr(), n, mpi.MPI_FLOAT, mpi.MPI_SUM) == 0
+    got = tio.cpu().numpy().view(np.uint32)
+    assert np.array_equal(got, want.view(np.uint32)), int(np.count_nonzero(got != want.view(np.uint32)))
+
+
+def _staged(torch, blocks):
+    """The blocks at coll_hip.c's staging stride (slot rounded to 256 B, + 4352 B
+    from 1 MiB up), as the all-to-all leaves them."""
+    nb = blocks[0].nbytes
+    stride = ((nb + 255) & ~255) + (4352 if nb >= MIB else 0)
+    buf = torch.zeros(stride * len(blocks), dtype=torch.uint8, device="cuda")
+    for j, blk in enumerate(blocks):
+        buf[j * stride:j * stride + nb] = torch.from_numpy(blk.view(np.uint8))
+    return buf, [buf.data_ptr() + j * stride for j in range(len(blocks))]
+
+
+def test_config4_tree8_fp32_32mib_blocks_vs_oracle(mpi, orc, cuda):
+    torch = cuda
+    n = (32 * MIB) // 4
+    rng = np.random.default_rng(4)
+    ys = [rng.uniform(-1, 1, n).astype(np.float32) for _ in range(8)]
+    buf, ptrs = _staged(torch, ys)
+    out = torch.empty(n * 4, dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
+    rc = mpi.reduce_local_multi(ptrs, out.data_ptr(), n, mpi.MPI_FLOAT, mpi.MPI_SUM, mpi.MPIX_ORDER_TREE)
+    assert rc == 0, mpi.error_string(rc)
+    torch.cuda.synchronize()
+    # ((y0+y1)+(y2+y3))+((y4+y5)+(y6+y7)), each + an MPIR_Reduce_local(in, inout)
+    # with inout the left operand
+    lvl = [y.copy() for y in ys]
+    while len(lvl) > 1:
+        nxt = []
+        for i in range(0, len(lvl), 2):
+            acc = lvl[i].copy()
+            assert orc.reduce_local(lvl[i + 1], acc, n, mpi.MPI_FLOAT, mpi.MPI_SUM) == 0
+            nxt.append(acc)
+        lvl = nxt
+    got = out.cpu().numpy().view(np.uint32)
+    assert np.array_equal(got, lvl[0].view(np.uint32)), int(np.count_nonzero(got != lvl[0].view(np.uint32)))
+
+
+def test_config5_chain8_fp16_128mib_blocks_vs_oracle(mpi, orc, cuda):
+    torch = cuda
+    n = (128 * MIB) // 2
+    rng = np.random.default_rng(5)
+    xs = [rng.uniform(-1, 1, n).astype(np.float16) for _ in range(8)]
+    buf, ptrs = _staged(torch, xs)
+    out = torch.empty(n * 2, dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
+    rc = mpi.reduce_local_multi(ptrs, out.data_ptr(), n, mpi.MPIX_C_FLOAT16, mpi.MPI_SUM, mpi.MPIX_ORDER_CHAIN)
+    assert rc == 0, mpi.error_string(rc)
+    torch.cuda.synchronize()
+    acc = xs[0].copy()
+    for j in range(1, 8):     # rounding to fp16 at every step, as the reference's loop does
+        assert orc.reduce_local(xs[j], acc, n, mpi.MPIX_C_FLOAT16, mpi.MPI_SUM) == 0
+    got = out.cpu().numpy().view(np.uint16)
+    assert np.array_equal(got, acc.view(np.uint16)), int(np.count_nonzero(got != acc.view(np.uint16)))
