@@ -212,18 +212,40 @@ def run_collectives_child(rank: int, world: int, local: int, barrier, timeout: f
     return {}
 
 
+def time_loop(run, k: int, w: int, sync, barrier, max_over_ranks, own: list | None = None) -> float:
+    """time_steps for a C loop: run(start, n) makes steps start .. start + n - 1
+    back to back; W untimed steps, then exactly K timed ones between barrier +
+    device sync, max over ranks."""
+    run(0, w)
+    sync()
+    barrier()
+    sync()
+    t0 = time.perf_counter()
+    run(w, k)
+    sync()
+    t1 = time.perf_counter()
+    barrier()
+    if own is not None:
+        own.append(t1 - t0)
+    return max_over_ranks(t1 - t0)
+
+
 def sync_loops(m, lib, reduce_local, ptrs, count, k: int, w: int, sync, barrier, max_over_ranks,
-               own: list | None = None):
+               own: list | None = None, c_loop=None):
     """The headline loop (NPAIRS pairs rotated: every call after the first
     NPAIRS repeats its kernel arguments, which the direct dispatch's kernarg
     cache then holds) and the same loop with fresh arguments on every call: the
     pairs shifted by multiples of 256 B (same count, same alignment, same
     kernel), 1024 distinct argument sets, so every call writes its arguments
     into a VRAM slot (before ringing the doorbell, for the checked kernel).
-    Returns seconds of each and the kernarg writes per timed fresh call."""
+    With `c_loop` (the compiled binding's reduce_local_loop) the K calls run
+    back to back in C, as a C caller issues them; the same loop stepped from
+    Python, one compiled call per step, is timed last (`dt_py`).
+    Returns seconds of each, the kernarg writes per timed fresh call, a
+    one-call step function and dt_py (None without c_loop)."""
     dt_f32, op_sum = m.MPI_FLOAT, m.MPI_SUM
-    call_args = [(pin, pio, count, dt_f32, op_sum) for pin, pio in ptrs]
-    fresh_args = [(pin + o, pio + o, count, dt_f32, op_sum) for o in range(0, SLACK, 256) for pin, pio in ptrs]
+    call_args = tuple((pin, pio, count, dt_f32, op_sum) for pin, pio in ptrs)
+    fresh_args = tuple((pin + o, pio + o, count, dt_f32, op_sum) for o in range(0, SLACK, 256) for pin, pio in ptrs)
 
     def step(i):
         rc = reduce_local(*call_args[i % NPAIRS])
@@ -234,11 +256,26 @@ def sync_loops(m, lib, reduce_local, ptrs, count, k: int, w: int, sync, barrier,
         rc = reduce_local(*fresh_args[i % len(fresh_args)])
         if rc:
             raise RuntimeError(m.error_string(rc))
-    dt = time_steps(step, k, w, sync, barrier, max_over_ranks, own)
-    kw0 = lib.MPIR_Hip_direct_kernarg_writes()
-    dtf = time_steps(fstep, k, w, sync, barrier, max_over_ranks, own)
-    writes = (lib.MPIR_Hip_direct_kernarg_writes() - kw0) / (k + w)
-    return dt, dtf, writes, step
+
+    def runner(sets):
+        def run(start, n):
+            rc = c_loop(sets, start, n)
+            if rc:
+                raise RuntimeError(m.error_string(rc))
+        return run
+    dt_py = None
+    if c_loop is not None:
+        dt = time_loop(runner(call_args), k, w, sync, barrier, max_over_ranks, own)
+        kw0 = lib.MPIR_Hip_direct_kernarg_writes()
+        dtf = time_loop(runner(fresh_args), k, w, sync, barrier, max_over_ranks, own)
+        writes = (lib.MPIR_Hip_direct_kernarg_writes() - kw0) / (k + w)
+        dt_py = time_steps(step, k, w, sync, barrier, max_over_ranks)
+    else:
+        dt = time_steps(step, k, w, sync, barrier, max_over_ranks, own)
+        kw0 = lib.MPIR_Hip_direct_kernarg_writes()
+        dtf = time_steps(fstep, k, w, sync, barrier, max_over_ranks, own)
+        writes = (lib.MPIR_Hip_direct_kernarg_writes() - kw0) / (k + w)
+    return dt, dtf, writes, step, dt_py
 
 
 def process_env(name: str) -> str:
@@ -267,8 +304,9 @@ def variant_child(args) -> None:
               (torch.rand(count + SLACK // 4, device="cuda", generator=g) * 2 - 1)) for _ in range(NPAIRS)]
     torch.cuda.synchronize()
     ptrs = [(a.data_ptr(), b.data_ptr()) for a, b in pairs]
-    dt, dtf, writes, _ = sync_loops(m, lib, reduce_local, ptrs, count, args.steps, args.warmup,
-                                    torch.cuda.synchronize, lambda: None, lambda x: x)
+    dt, dtf, writes, _, _ = sync_loops(m, lib, reduce_local, ptrs, count, args.steps, args.warmup,
+                                       torch.cuda.synchronize, lambda: None, lambda x: x,
+                                       c_loop=m.fast_reduce_local_loop())
     print(json.dumps({"dt": dt, "dt_fresh": dtf, "kernarg_writes_per_fresh_call": writes,
                       "HSA_ALLOCATE_QUEUE_DEV_MEM": process_env("HSA_ALLOCATE_QUEUE_DEV_MEM"),
                       "direct_state": lib.MPIR_Hip_direct_state(0)}), flush=True)
@@ -714,17 +752,21 @@ def main():
     ptrs = [(a.data_ptr(), b.data_ptr()) for a, b in pairs]
     sync()
 
-    # MPI_Reduce_local through the compiled binding (csrc/py/fastcall.c), the
-    # way mpi4py calls MPI: ~0.25 us of Python per call instead of ~1.2 us (ctypes)
+    # MPI_Reduce_local from C, K calls back to back (the compiled binding's
+    # reduce_local_loop, csrc/py/fastcall.c), as a C caller -- an MPICH
+    # schedule, an OSU-style benchmark -- issues them; the same K calls stepped
+    # from Python (one compiled call per step, the way mpi4py calls MPI, ~0.25 us
+    # of Python each) are reported beside it (sync_variants.python_loop)
     try:
-        reduce_local, binding = m.fast_reduce_local(), "compiled CPython binding (csrc/py/fastcall.c)"
+        reduce_local, c_loop = m.fast_reduce_local(), m.fast_reduce_local_loop()
+        binding = "C loop of the compiled binding (csrc/py/fastcall.c reduce_local_loop)"
     except ImportError:     # extension not built: the same C entry point through ctypes
-        reduce_local, binding = lib.MPI_Reduce_local, "ctypes"
+        reduce_local, c_loop, binding = lib.MPI_Reduce_local, None, "ctypes"
     own = []
     d_before = lib.MPIR_Hip_direct_dispatches()
-    dt, dt_fresh, fresh_writes, step = sync_loops(m, lib, reduce_local, ptrs, count, args.steps, args.warmup,
-                                                  sync, barrier, max_over_ranks, own)
-    direct_share = (lib.MPIR_Hip_direct_dispatches() - d_before) / (2 * (args.steps + args.warmup))
+    dt, dt_fresh, fresh_writes, step, dt_py = sync_loops(m, lib, reduce_local, ptrs, count, args.steps,
+                                                         args.warmup, sync, barrier, max_over_ranks, own, c_loop)
+    direct_share = (lib.MPIR_Hip_direct_dispatches() - d_before) / ((3 if c_loop else 2) * (args.steps + args.warmup))
     value = alg_bytes * args.steps * world / dt / GIB
     # each rank's own figures beside the max-over-ranks `value`: a lagging GPU,
     # or a rank whose calls left the direct path, shows here
@@ -765,7 +807,9 @@ def main():
             "environment": "as launched: the bench sets no runtime variable; HSA_ALLOCATE_QUEUE_DEV_MEM is the "
                            "library's load-time default (1) unless the job sets it (config.runtime)",
             "kernel_arguments": "%d rotating pairs: every call after the first %d repeats its arguments (kernarg "
-                                "cache hit); sync_variants.fresh_args misses on every call" % (NPAIRS, NPAIRS)},
+                                "cache hit); sync_variants.fresh_args misses on every call" % (NPAIRS, NPAIRS),
+            "caller": "K synchronous MPI_Reduce_local calls back to back from C (" + binding + "); "
+                      "sync_variants.python_loop steps the same calls from Python"},
         # the synchronous call per GPU (launch + completion included) against the HBM peak
         "per_gpu": {"GiBps": round(value / world, 1),
                     "frac_of_hbm_peak": round(value / world * GIB / HBM_PEAK_BPS, 4),
@@ -783,6 +827,9 @@ def main():
     variants = {"fresh_args": dict(rate(dt_fresh), kernarg_writes_per_call=round(fresh_writes, 3),
                                    note="same loop, every call's arguments new (pairs shifted by multiples of "
                                         "256 B, 1024 distinct sets): kernarg BAR write + HDP flush per call")}
+    if dt_py is not None:
+        variants["python_loop"] = dict(rate(dt_py), note="the headline loop stepped from Python: one compiled-binding "
+                                                         "call per step (mpi4py's way), timed after the C loops")
     if ring_variant is not None:
         if "dt" in ring_variant:
             variants["rocm_ring_placement"] = {

@@ -40,9 +40,77 @@ static PyObject *fc_reduce_local(PyObject *self, PyObject *const *args, Py_ssize
     return PyLong_FromLong(rc);
 }
 
+/* reduce_local_loop(arg_sets, start, k) -> int: k MPI_Reduce_local calls in a
+ * C loop, call i with arg_sets[(start + i) % len(arg_sets)] (5-tuples as for
+ * reduce_local), the way a C caller -- an MPICH schedule, an OSU-style
+ * benchmark -- issues them: the k argument sets are unpacked first, then the
+ * calls run back to back without the GIL.  Returns the first nonzero error
+ * code (and stops there), else 0. */
+static PyObject *fc_reduce_local_loop(PyObject *self, PyObject *const *args, Py_ssize_t nargs)
+{
+    struct set {
+        const void *in;
+        void *io;
+        int count, dt, op;
+    } *sets;
+    Py_ssize_t n, start, k, i, m;
+    int rc = 0;
+    (void) self;
+    if (nargs != 3 || !PyTuple_Check(args[0])) {
+        PyErr_SetString(PyExc_TypeError, "reduce_local_loop(arg_sets: tuple of 5-tuples, start, k)");
+        return NULL;
+    }
+    n = PyTuple_GET_SIZE(args[0]);
+    start = PyLong_AsSsize_t(args[1]);
+    k = PyLong_AsSsize_t(args[2]);
+    if (PyErr_Occurred())
+        return NULL;
+    if (n < 1 || k < 0 || start < 0) {
+        PyErr_SetString(PyExc_ValueError, "need at least one argument set, k >= 0, start >= 0");
+        return NULL;
+    }
+    /* the m = min(n, k) distinct sets the calls use, in call order: call i
+     * takes sets[i % m] */
+    m = n < k ? n : k;
+    sets = PyMem_Malloc(sizeof(*sets) * (size_t) (m ? m : 1));
+    if (!sets)
+        return PyErr_NoMemory();
+    for (i = 0; i < m; i++) {
+        PyObject *t = PyTuple_GET_ITEM(args[0], (start + i) % n);
+        long count;
+        if (!PyTuple_Check(t) || PyTuple_GET_SIZE(t) != 5) {
+            PyMem_Free(sets);
+            PyErr_SetString(PyExc_TypeError, "each argument set is (inbuf, inoutbuf, count, datatype, op)");
+            return NULL;
+        }
+        sets[i].in = PyLong_AsVoidPtr(PyTuple_GET_ITEM(t, 0));
+        sets[i].io = PyLong_AsVoidPtr(PyTuple_GET_ITEM(t, 1));
+        count = PyLong_AsLong(PyTuple_GET_ITEM(t, 2));
+        sets[i].dt = (int) PyLong_AsLong(PyTuple_GET_ITEM(t, 3));
+        sets[i].op = (int) PyLong_AsLong(PyTuple_GET_ITEM(t, 4));
+        if (PyErr_Occurred() || count < INT_MIN || count > INT_MAX) {
+            PyMem_Free(sets);
+            if (!PyErr_Occurred())
+                PyErr_SetString(PyExc_OverflowError, "count does not fit the C int of MPI_Reduce_local");
+            return NULL;
+        }
+        sets[i].count = (int) count;
+    }
+    Py_BEGIN_ALLOW_THREADS
+    for (i = 0; i < k && rc == 0; i++) {
+        const struct set *s = &sets[i % m];
+        rc = MPI_Reduce_local(s->in, s->io, s->count, (MPI_Datatype) s->dt, (MPI_Op) s->op);
+    }
+    Py_END_ALLOW_THREADS
+    PyMem_Free(sets);
+    return PyLong_FromLong(rc);
+}
+
 static PyMethodDef fc_methods[] = {
     {"reduce_local", (PyCFunction) (void (*)(void)) fc_reduce_local, METH_FASTCALL,
      "MPI_Reduce_local(inbuf, inoutbuf, count, datatype, op) on raw addresses; returns the MPI error code"},
+    {"reduce_local_loop", (PyCFunction) (void (*)(void)) fc_reduce_local_loop, METH_FASTCALL,
+     "k MPI_Reduce_local calls in a C loop over arg_sets[(start + i) % len]; returns the first error code"},
     {NULL, NULL, 0, NULL}
 };
 

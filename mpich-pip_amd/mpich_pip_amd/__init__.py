@@ -240,6 +240,15 @@ def fast_reduce_local():
     return _fastcall.reduce_local
 
 
+def fast_reduce_local_loop():
+    """f(arg_sets, start, k) -> error code: k MPI_Reduce_local calls in a C loop
+    (csrc/py/fastcall.c), call i with arg_sets[(start + i) % len(arg_sets)], the
+    way a C caller issues them.  Raises if the extension was not built."""
+    load()
+    from . import _fastcall
+    return _fastcall.reduce_local_loop
+
+
 def reduce_local(inbuf: int, inoutbuf: int, count: int, datatype: int, op: int) -> int:
     """MPI_Reduce_local on raw addresses (device or host)."""
     return load().MPI_Reduce_local(ctypes.c_void_p(inbuf), ctypes.c_void_p(inoutbuf), count, datatype, op)
