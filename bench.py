@@ -56,6 +56,7 @@ from __future__ import annotations
 
 import argparse
 import ctypes
+import gc
 import json
 import os
 import sys
@@ -158,17 +159,24 @@ def cpu_standin(args) -> None:
 
 def time_steps(step, k: int, w: int, sync, barrier, max_over_ranks, own: list | None = None) -> float:
     """W untimed steps, then exactly K steps bracketed by barrier + device sync; max over ranks.
-    `own`, if given, receives this rank's own seconds (for the per-rank report)."""
+    `own`, if given, receives this rank's own seconds (for the per-rank report).
+    Python's cyclic garbage collector is held off while the K steps run, as
+    timeit does: a full collection over torch's objects can take milliseconds,
+    which the Python-stepped loops would otherwise count as a step."""
     for i in range(w):
         step(i)
     sync()
     barrier()
     sync()
+    gc_on = gc.isenabled()
+    gc.disable()
     t0 = time.perf_counter()
     for i in range(k):
         step(w + i)
     sync()
     t1 = time.perf_counter()
+    if gc_on:
+        gc.enable()
     barrier()
     if own is not None:
         own.append(t1 - t0)
