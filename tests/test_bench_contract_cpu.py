@@ -1,4 +1,4 @@
-"""The committed bench line (profiles/archive/r03/r03_bench.log, measured on MI355X) against
+"""The committed bench line (profiles/r04/bench_r04final.log, measured on MI355X) against
 the driver's contract and against itself: BASELINE.json's metric, the
 required keys, value = algorithmic bytes x N / time, roofline.frac =
 achieved / peak with achieved = 805,306,368 B / mean launch time, and the
@@ -10,7 +10,7 @@ import os
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LINE = os.path.join(ROOT, "profiles", "archive", "r03", "r03_bench.log")
+LINE = os.path.join(ROOT, "profiles", "r04", "bench_r04final.log")
 GIB = float(1 << 30)
 
 
@@ -62,10 +62,24 @@ def test_roofline_is_self_consistent(line):
 
 def test_live_kernel_time_agrees_with_rocprof(line):
     """bench.py times the kernel the synchronous call runs; rocprofv3's
-    --kernel-trace --stats average for that kernel (profiles/archive/r03/r03_kernel_stats.csv,
+    --kernel-trace --stats average for that kernel (profiles/r04/r04_kernel_stats.csv,
     summarised in pmc_traffic.json) must agree with it."""
     r = line["roofline"]
     with open(os.path.join(ROOT, "profiles", "pmc_traffic.json")) as f:
         pmc = json.load(f)
     assert "mpir_tile_SUM_MPIR_HIP_F32" in r["kernel"] and "mpir_tile_SUM_MPIR_HIP_F32" in pmc["kernel"]
     assert r["mean_launch_us"] == pytest.approx(pmc["rocprof_avg_launch_ns"] * 1e-3, rel=0.05)
+
+
+def test_per_rank_and_config5_blocks(line):
+    """Round 4: every rank's own loop beside value (value's time is the slowest
+    rank's), and config 5's fp16 combine with its PMC traffic."""
+    pr = line["per_rank"]
+    assert [r["rank"] for r in pr] == list(range(line["n_gpus"]))
+    assert max(r["seconds"] for r in pr) * 1e3 / line["steps"] == pytest.approx(line["ms_per_step"], rel=2e-3)
+    assert all(r["direct_state"] in (1, 2) and r["direct_share"] == 1.0 for r in pr)
+    c5 = line["config5_combine"]
+    for key, alg in (("two_operand", 3 * 256 * (1 << 20)), ("chain8", 9 * 128 * (1 << 20))):
+        b = c5[key]
+        assert b["frac"] == pytest.approx(alg / (b["kernel_us"] * 1e-6) / 8.0e12, rel=2e-3)
+        assert 1.0 <= b["traffic_over_algorithmic"] < 1.01

@@ -111,10 +111,17 @@ def main():
                 r = dict(r)
                 r["Name"] = short(r["Name"])
                 w.writerow(r)
-    json.dump(d, open(os.path.join(prof, "pmc_traffic.json"), "w"), indent=1)
+    # keep the other kernels' entries (config5_fp16, tools/summarize_config5.py)
+    pj = os.path.join(prof, "pmc_traffic.json")
+    if os.path.exists(pj):
+        old = json.load(open(pj))
+        for k in ("config5_fp16",):
+            if k in old:
+                d[k] = old[k]
+    json.dump(d, open(pj, "w"), indent=1)
     with open(os.path.join(prof, f"{tag}_summary.md"), "w") as f:
         f.write(f"# rocprofv3 summary ({tag})\n\n")
-        f.write(f"Command: `bash tools/profile_{tag[:3]}.sh` on one MI355X "
+        f.write(f"Command: `bash {os.environ.get('PROFILE_SCRIPT', 'tools/profile_r03.sh')}` on one MI355X "
                 "(bench.py --no-cpu-baseline --no-extras: fp32 MPI_SUM, 256 MiB per operand).\n\n")
         f.write("| quantity | value |\n|---|---|\n")
         f.write(f"| kernel | `{d['kernel']}` |\n")
