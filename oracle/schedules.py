@@ -161,17 +161,27 @@ def allreduce_rsag(rank_bufs: list[np.ndarray], count: int, esz: int, dt: int, o
 
 
 def reduce_scatter_block_pairwise(rank_sendbufs: list[np.ndarray], recvcount: int, esz: int, dt: int,
-                                  op: int) -> list[np.ndarray]:
-    """Each rank's recvbuf after MPI_Reduce_scatter_block (pairwise exchanges)."""
+                                  op: int, workers: int = 1) -> list[np.ndarray]:
+    """Each rank's recvbuf after MPI_Reduce_scatter_block (pairwise exchanges).
+    Rank r's block is its own chain ((x_r + x_{r-1}) + x_{r-2}) + ..., independent
+    of the other ranks', so `workers` > 1 runs the ranks' chains on that many
+    threads (the oracle's C calls release the GIL); each chain keeps its order."""
     p = len(rank_sendbufs)
     send = [b.view(np.uint8).reshape(-1) for b in rank_sendbufs]
     nb = recvcount * esz
     recv = [send[r][r * nb:(r + 1) * nb].copy() for r in range(p)]
-    for i in range(1, p):
-        for r in range(p):
+
+    def chain(r):
+        for i in range(1, p):
             src = (r - i + p) % p
-            tmp = send[src][r * nb:(r + 1) * nb].copy()
-            _red(tmp, recv[r], recvcount, dt, op)
+            _red(send[src][r * nb:(r + 1) * nb].copy(), recv[r], recvcount, dt, op)
+    if workers > 1:
+        from concurrent.futures import ThreadPoolExecutor
+        with ThreadPoolExecutor(workers) as ex:
+            list(ex.map(chain, range(p)))
+    else:
+        for r in range(p):
+            chain(r)
     return recv
 
 

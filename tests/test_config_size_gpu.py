@@ -103,3 +103,83 @@ def test_config5_chain8_fp16_128mib_blocks_vs_oracle(mpi, orc, cuda):
         assert orc.reduce_local(xs[j], acc, n, mpi.MPIX_C_FLOAT16, mpi.MPI_SUM) == 0
     got = out.cpu().numpy().view(np.uint16)
     assert np.array_equal(got, acc.view(np.uint16)), int(np.count_nonzero(got != acc.view(np.uint16)))
+
+
+# ---- configs 4 and 5 end to end at 8 ranks and full size, on one GPU: the
+# ---- loopback communicator (8 virtual ranks, one host thread each, transfers
+# ---- are device copies) runs the complete reference-order collective -- the
+# ---- all-to-all of blocks into the skewed staging slots, the fused combine,
+# ---- the allgather -- on the BASELINE workload.  Only the transport differs
+# ---- from the 8-GPU run (grouped ncclSend / ncclRecv over xGMI,
+# ---- tests/test_coll_rccl_gpu.py).
+
+def test_config4_allreduce_fp32_256mib_8_ranks_loopback_vs_oracle(mpi, orc, cuda):
+    """MPI_Allreduce fp32 SUM, 256 MiB per rank, 8 ranks: MPICH's choice on one
+    node (allreduce_intra_smp.c -> reduce_intra_reduce_scatter_gather.c:186-249,
+    then the bcast), oracle/schedules.py allreduce_smp_auto step by step."""
+    from oracle import schedules as S
+    from test_coll_loopback_gpu import run_ranks
+    torch = cuda
+    p, count = 8, (256 * MIB) // 4
+    xs = [np.random.default_rng(400 + r).uniform(-1, 1, count).astype(np.float32) for r in range(p)]
+    want = S.allreduce_smp_auto(xs, count, 4, mpi.MPI_FLOAT, mpi.MPI_SUM).view(np.uint32)
+    comms = mpi.comm_create_loopback(p)
+    try:
+        send = [torch.from_numpy(x).cuda() for x in xs]
+        del xs
+        recv = [torch.empty_like(s) for s in send]
+        torch.cuda.synchronize()
+
+        def rank(r):
+            rc = mpi.allreduce(send[r].data_ptr(), recv[r].data_ptr(), count, mpi.MPI_FLOAT, mpi.MPI_SUM, comms[r],
+                               mpi.MPIX_HIP_ALG_REFERENCE_ORDER)
+            assert rc == 0, mpi.error_string(rc)
+
+        run_ranks(rank, p)
+        torch.cuda.synchronize()
+        for r in range(p):
+            got = recv[r].cpu().numpy().view(np.uint32)
+            assert np.array_equal(got, want), f"rank {r}: {int(np.count_nonzero(got != want))} elements differ"
+    finally:
+        for c in comms:
+            mpi.comm_free(c)
+
+
+def test_config5_reduce_scatter_block_fp16_1gib_8_ranks_loopback_vs_oracle(mpi, orc, cuda):
+    """MPI_Reduce_scatter_block fp16 SUM, 1 GiB sendbuf per rank (recvcount
+    2^29 / 8), 8 ranks: pairwise (reduce_scatter_block.c:136-148,
+    reduce_scatter_block_intra_pairwise.c:97-134), oracle/schedules.py
+    reduce_scatter_block_auto's chain per rank, rounded to fp16 at every step.
+    Operands: random fp16 bit patterns of magnitude < 2 (subnormals and zeros
+    included), so the 8-term sums stay finite."""
+    from oracle import schedules as S
+    from test_coll_loopback_gpu import run_ranks
+    torch = cuda
+    p = 8
+    total = (1024 * MIB) // 2
+    rcount = total // p
+    xs = [np.random.default_rng(500 + r).integers(0, 1 << 16, total, dtype=np.uint16) & np.uint16(0xBFFF)
+          for r in range(p)]
+    assert p * rcount * 2 >= S.RSB_COMMUTATIVE_LONG_MSG_SIZE      # the pairwise algorithm
+    want = S.reduce_scatter_block_pairwise(xs, rcount, 2, mpi.MPIX_C_FLOAT16, mpi.MPI_SUM, workers=p)
+    comms = mpi.comm_create_loopback(p)
+    try:
+        send = [torch.from_numpy(x.view(np.int16)).cuda() for x in xs]
+        del xs
+        recv = [torch.empty(rcount, dtype=torch.int16, device="cuda") for _ in range(p)]
+        torch.cuda.synchronize()
+
+        def rank(r):
+            rc = mpi.reduce_scatter_block(send[r].data_ptr(), recv[r].data_ptr(), rcount, mpi.MPIX_C_FLOAT16,
+                                          mpi.MPI_SUM, comms[r], mpi.MPIX_HIP_ALG_REFERENCE_ORDER)
+            assert rc == 0, mpi.error_string(rc)
+
+        run_ranks(rank, p)
+        torch.cuda.synchronize()
+        for r in range(p):
+            got = recv[r].cpu().numpy().view(np.uint16)
+            w = want[r].view(np.uint16)
+            assert np.array_equal(got, w), f"rank {r}: {int(np.count_nonzero(got != w))} elements differ"
+    finally:
+        for c in comms:
+            mpi.comm_free(c)
