@@ -30,7 +30,7 @@
 //   * work the caller queued on the legacy null stream for these buffers stays
 //     ordered before the reduction, as with the blocking HIP stream: when
 //     hipStreamQuery(NULL) reports pending work (it keeps doing so for finished
-//     work until the host synchronises, tools/direct_probe.py), the call first
+//     work until the host synchronises, tools/archive/direct_probe.py), the call first
 //     synchronises with the null stream;
 //   * the calling thread has no unfinished work on its own library stream.
 // Packets carry an agent-scope acquire (what HIP uses between kernels; a
@@ -199,9 +199,9 @@ int mode() {
 
 // The calls' queue records no dispatch timestamps: with them the CP's
 // per-packet timestamp writes cost the synchronous call ~0.4 us at 256 MiB and
-// ~0.9 us at 64 MiB (alternated processes, tools/ts_ab.sh, profiles/archive/r02/ts_ab.log),
+// ~0.9 us at 64 MiB (alternated processes, tools/archive/ts_ab.sh, profiles/archive/r02/ts_ab.log),
 // and switching them on for a live queue does not take effect
-// (tools/ts_enable_probe.py).  A second queue, created with them on, takes the
+// (tools/archive/ts_enable_probe.py).  A second queue, created with them on, takes the
 // calls made while MPIR_Hip_direct_profile is on (the bench's roofline readout:
 // the same kernel object, plan and arguments).
 //
@@ -209,7 +209,7 @@ int mode() {
 // system-scope acquire costs ~7 us of kernel body, aql_sig_nt_sys) and
 // system-scope release, so the result is visible to every agent -- SDMA copies
 // and the host included -- when the signal fires.  Other scopes measured within
-// 0.2 us (tools/scope_ab.sh, profiles/archive/r02/scope_ab.log); none at release would
+// 0.2 us (tools/archive/scope_ab.sh, profiles/archive/r02/scope_ab.log); none at release would
 // leave results in one XCD's L2 and is not offered.
 constexpr int kAcquireScope = HSA_FENCE_SCOPE_AGENT;
 constexpr int kReleaseScope = HSA_FENCE_SCOPE_SYSTEM;
@@ -639,7 +639,7 @@ int direct_reduce(int dev, int op, int elem, const ReducePlan &p, int *rc) {
     // Work queued on the legacy null stream stays ordered before us, as it is
     // for the HIP path's blocking library stream.  hipStreamQuery(nullptr)
     // keeps answering "not ready" after such work has finished until the host
-    // synchronises with it (measured: tools/direct_probe.py), so a busy answer
+    // synchronises with it (measured: tools/archive/direct_probe.py), so a busy answer
     // is followed by that synchronisation -- the wait the synchronous call
     // would spend behind the same work on the HIP path anyway.
     if (hipStreamQuery(nullptr) != hipSuccess) {

@@ -81,7 +81,7 @@ constexpr int kMaxStageSlots = 8;
 // `stage_slots()` device scratch slots, so host->device and device->host
 // transfers run at the same time (PCIe is full duplex).  Events order the
 // stages of one chunk and stop a slot from being refilled before its
-// copy-back has read it.  Defaults 16 MiB x 3 slots (tools/stage_sweep.py,
+// copy-back has read it.  Defaults 16 MiB x 3 slots (tools/archive/stage_sweep.py,
 // profiles/archive/r01s3_stage_sweep.log: pinned 71.8 GiB/s, pageable 66.3 with the
 // bounce path below; 32 MiB chunks leave a longer tail of copy-outs).
 // MPIR_CVAR_REDUCE_LOCAL_STAGE_CHUNK_MB / MPIR_CVAR_REDUCE_LOCAL_STAGE_SLOTS override.

@@ -43,7 +43,7 @@ constexpr int kCachePolicySC1 = 16;                           // aux bit: sc1 (d
 // Infinity Cache (MALL), an nt store bypasses it; so a result of at most 64 MiB
 // stays there for its next reader (the next schedule step, the RCCL send of a
 // block, the D2H copy of a staged chunk): 64 MiB re-read within ~256 MiB of
-// traffic 27.0 vs 33.2 us (tools/sync_store_ab.hip,
+// traffic 27.0 vs 33.2 us (tools/archive/sync_store_ab.hip,
 // profiles/archive/r01s4_sync_store_ab.log).  With nothing re-read the two policies
 // are within noise at <= 64 MiB, and at 256 MiB sc1 on any part of the result
 // costs ~1 us (profiles/archive/r02/pairs_ab.log: a "last 64 MiB sc1" variant only won
@@ -134,7 +134,7 @@ __device__ __forceinline__ void issue_gap() {
 // start off a 16 KiB boundary otherwise put every tile across two 16 KiB
 // blocks, every wave's 4 KiB across two 4 KiB blocks (and at 64 B off, every
 // 1 KiB access across nine 128 B lines instead of eight): measured at 256 MiB
-// (tools/align_sweep.py, profiles/r03/align_sweep.log), both operands 64 B /
+// (tools/archive/align_sweep.py, profiles/archive/r03/align_sweep.log), both operands 64 B /
 // 4 KiB / 8 KiB off a 2 MiB boundary took 125.0 / 124.0 / 128.5 us against
 // 120.8 us aligned.  Tile 0 is then the partial block up to the first
 // boundary: its lanes below the cut get offsets that wrap past the buffer

@@ -1083,7 +1083,7 @@ def test_direct_dispatch_orders_after_null_stream(mpi, cuda):
     is finished before the reduction reads them: the direct path first
     synchronises with a null stream that reports pending work, then dispatches
     (hipStreamQuery(nullptr) alone keeps reporting finished work as pending
-    until the host synchronises, tools/direct_probe.py)."""
+    until the host synchronises, tools/archive/direct_probe.py)."""
     torch = cuda
     if torch.cuda.current_stream().cuda_stream != 0:
         pytest.skip("torch's current stream is not the legacy null stream")
