@@ -713,6 +713,30 @@ __global__ __launch_bounds__(kThreads) void k_combine_multi_elems(MultiArgs a, u
     }
 }
 
+// Eight operands on 1024-thread workgroups run one workgroup per CU: a dynamic
+// LDS reservation the kernel never touches (more than half of the CU's 160 KiB)
+// leaves room for one instead of two, so 128 KiB of loads are in flight per CU
+// instead of 256.  Eight read streams plus one write stream move ~1 point of
+// peak faster that way (the eight reads alone do not: the write stream is what
+// gains), in every alternated pair measured with the library's own kernel:
+// TREE8 fp32 over 8 x 32 MiB 0.744 -> 0.753 (sc1 stores) and 0.754 -> 0.765 (nt),
+// CHAIN8 fp16 over 8 x 128 MiB 0.745 -> 0.761 and 0.776 -> 0.779
+// (tools/multi_occ_ab.hip, profiles/r04/multi_occ_ab*.log; XOR folds in
+// tools/fused_write_ab.hip, profiles/r04/fused_write_ab.log, fused_occ_sweep.log).
+// 0 (no reservation) if the runtime refuses the attribute.
+constexpr int kMultiCapLds = 96 << 10;
+template <class Op, class T, int P, bool TREE, int U, int TH>
+size_t multi_lds_cap() {
+    if constexpr (P < 8 || TH != 1024) {
+        return 0;
+    } else {
+        static const size_t v = hipFuncSetAttribute((const void *)k_combine_multi<Op, T, P, TREE, U, TH>,
+                                                    hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                    kMultiCapLds) == hipSuccess ? (size_t)kMultiCapLds : 0;
+        return v;
+    }
+}
+
 template <class Op, class T, int P, bool TREE, int U, int TH>
 hipError_t launch_combine_pu(const void *const *ins, void *out_, uint64_t count, hipStream_t s) {
     constexpr uint32_t tile = TH * U * 16;
@@ -740,7 +764,8 @@ hipError_t launch_combine_pu(const void *const *ins, void *out_, uint64_t count,
         a.tail_off = (int64_t)vbytes;
         uint64_t grid = (vbytes + tile - 1) / tile;
         if (grid == 0) grid = 1;
-        hipLaunchKernelGGL((k_combine_multi<Op, T, P, TREE, U, TH>), dim3((unsigned)grid), dim3(TH), 0, s, a);
+        const size_t lds = multi_lds_cap<Op, T, P, TREE, U, TH>();
+        hipLaunchKernelGGL((k_combine_multi<Op, T, P, TREE, U, TH>), dim3((unsigned)grid), dim3(TH), lds, s, a);
     } else {
         a.out = out;
         a.vbytes = 0;
