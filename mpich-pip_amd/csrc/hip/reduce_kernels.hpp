@@ -724,10 +724,13 @@ __global__ __launch_bounds__(kThreads) void k_combine_multi_elems(MultiArgs a, u
 // (tools/multi_occ_ab.hip, profiles/r04/multi_occ_ab*.log; XOR folds in
 // tools/fused_write_ab.hip, profiles/r04/fused_write_ab.log, fused_occ_sweep.log).
 // 0 (no reservation) if the runtime refuses the attribute.
-constexpr int kMultiCapLds = 96 << 10;
+#ifndef MPIR_MULTI_CAP_LDS
+#define MPIR_MULTI_CAP_LDS (96 << 10)    // (a build-time override for tools/multi_cap_ab.sh only)
+#endif
+constexpr int kMultiCapLds = MPIR_MULTI_CAP_LDS;
 template <class Op, class T, int P, bool TREE, int U, int TH>
 size_t multi_lds_cap() {
-    if constexpr (P < 8 || TH != 1024) {
+    if constexpr (P < 8 || TH != 1024 || kMultiCapLds == 0) {
         return 0;
     } else {
         static const size_t v = hipFuncSetAttribute((const void *)k_combine_multi<Op, T, P, TREE, U, TH>,
