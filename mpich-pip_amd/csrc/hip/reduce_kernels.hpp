@@ -713,29 +713,37 @@ __global__ __launch_bounds__(kThreads) void k_combine_multi_elems(MultiArgs a, u
     }
 }
 
-// Eight operands on 1024-thread workgroups run one workgroup per CU: a dynamic
-// LDS reservation the kernel never touches (more than half of the CU's 160 KiB)
-// leaves room for one instead of two, so 128 KiB of loads are in flight per CU
-// instead of 256.  Eight read streams plus one write stream move ~1 point of
-// peak faster that way (the eight reads alone do not: the write stream is what
-// gains), in every alternated pair measured with the library's own kernel:
-// TREE8 fp32 over 8 x 32 MiB 0.744 -> 0.753 (sc1 stores) and 0.754 -> 0.765 (nt),
-// CHAIN8 fp16 over 8 x 128 MiB 0.745 -> 0.761 and 0.776 -> 0.779
-// (tools/multi_occ_ab.hip, profiles/r04/multi_occ_ab*.log; XOR folds in
-// tools/fused_write_ab.hip, profiles/r04/fused_write_ab.log, fused_occ_sweep.log).
+// Fewer loads in flight per CU for the many-operand folds: a dynamic LDS
+// reservation the kernel never touches caps the workgroups a CU holds.
+//   * P = 8 (1024-thread workgroups): 96 KiB, one per CU instead of two, 128 KiB
+//     of loads in flight per CU instead of 256.  The eight reads alone do not
+//     gain: the write stream among them does (tools/fused_write_ab.hip,
+//     tools/multi_occ_ab.hip, profiles/r04/fused_*.log, multi_occ_ab*.log).
+//   * P = 4 (256 threads x 4 vectors): 53 KiB, three per CU (192 KiB in flight;
+//     shape sweep: tools/multi_p24_occ_ab.hip, profiles/r04/multi_p24_occ_ab.log).
+//   * P = 2: no cap (TREE2 loses 2 points under one, CHAIN2 moves by 0.3).
+// Two library builds alternated (tools/multi_cap_ab.sh, profiles/r04/
+// multi_cap_ab.log, four pairs per case, outputs identical), without -> with:
+// TREE8 fp32 over 8 x 32 MiB 0.744-0.749 -> 0.750-0.757, CHAIN8 fp16 over
+// 8 x 128 MiB 0.745-0.749 -> 0.762-0.764, TREE4 fp32 over 4 x 64 MiB
+// 0.726-0.735 -> 0.756-0.758, CHAIN4 fp16 over 4 x 256 MiB 0.760-0.763 -> 0.809-0.813.
 // 0 (no reservation) if the runtime refuses the attribute.
 #ifndef MPIR_MULTI_CAP_LDS
-#define MPIR_MULTI_CAP_LDS (96 << 10)    // (a build-time override for tools/multi_cap_ab.sh only)
+#define MPIR_MULTI_CAP_LDS 1    // 0: no reservation (a build-time override for tools/multi_cap_ab.sh only)
 #endif
-constexpr int kMultiCapLds = MPIR_MULTI_CAP_LDS;
+template <int P, int TH>
+constexpr int multi_cap_bytes() {
+    return !MPIR_MULTI_CAP_LDS ? 0 : (P == 8 && TH == 1024) ? (96 << 10) : (P == 4 && TH == kThreads) ? (53 << 10) : 0;
+}
 template <class Op, class T, int P, bool TREE, int U, int TH>
 size_t multi_lds_cap() {
-    if constexpr (P < 8 || TH != 1024 || kMultiCapLds == 0) {
+    constexpr int cap = multi_cap_bytes<P, TH>();
+    if constexpr (cap == 0) {
         return 0;
     } else {
         static const size_t v = hipFuncSetAttribute((const void *)k_combine_multi<Op, T, P, TREE, U, TH>,
                                                     hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                    kMultiCapLds) == hipSuccess ? (size_t)kMultiCapLds : 0;
+                                                    cap) == hipSuccess ? (size_t)cap : 0;
         return v;
     }
 }

@@ -1,14 +1,15 @@
 #!/usr/bin/env python3
-"""The fused 8-operand combine through the library's own entry point
-(MPIX_Reduce_local_multi), one library build per process: the product (one
-1024-thread workgroup per CU, reduce_kernels.hpp multi_lds_cap) against a build
-with -DMPIR_MULTI_CAP_LDS=0 (two per CU, as before round 4).  Alternate the two
+"""The fused 8- and 4-operand combines through the library's own entry point
+(MPIX_Reduce_local_multi), one library build per process: the product (an LDS
+reservation capping the workgroups per CU, reduce_kernels.hpp multi_lds_cap)
+against a build with -DMPIR_MULTI_CAP_LDS=0 (no cap, as before round 4).  Alternate the two
 builds with tools/multi_cap_ab.sh.
 
     python3 tools/multi_cap_ab.py <dir holding libmpich_reduce_local.so> [--rounds 6]
 
 Cases: config 4's TREE8 fp32 SUM over 8 x 32 MiB blocks and config 5's CHAIN8
-fp16 SUM over 8 x 128 MiB, blocks at the collective's staging stride (+4352 B),
+fp16 SUM over 8 x 128 MiB (8 ranks), TREE4 over 4 x 64 MiB and CHAIN4 over
+4 x 256 MiB (4 ranks), blocks at the collective's staging stride (+4352 B),
 operand sets rotated past the Infinity Cache; HIP events around batches of 20
 back-to-back launches on one stream; median us per launch and fraction of
 8 TB/s per round.  The first launch's output is hashed so the two builds can be
@@ -37,16 +38,18 @@ def main():
     tag = os.path.basename(os.path.abspath(args.libdir))
     st = torch.cuda.Stream()
     g = torch.Generator(device="cuda").manual_seed(0xCA9)
-    for name, blk_bytes, dt, tdt, order in (
-            ("TREE8 fp32 8 x 32 MiB", 32 * MIB, m.MPI_FLOAT, torch.float32, m.MPIX_ORDER_TREE),
-            ("CHAIN8 fp16 8 x 128 MiB", 128 * MIB, m.MPIX_C_FLOAT16, torch.float16, m.MPIX_ORDER_CHAIN)):
+    for name, p, blk_bytes, dt, tdt, order in (
+            ("TREE8 fp32 8 x 32 MiB", 8, 32 * MIB, m.MPI_FLOAT, torch.float32, m.MPIX_ORDER_TREE),
+            ("CHAIN8 fp16 8 x 128 MiB", 8, 128 * MIB, m.MPIX_C_FLOAT16, torch.float16, m.MPIX_ORDER_CHAIN),
+            ("TREE4 fp32 4 x 64 MiB", 4, 64 * MIB, m.MPI_FLOAT, torch.float32, m.MPIX_ORDER_TREE),
+            ("CHAIN4 fp16 4 x 256 MiB", 4, 256 * MIB, m.MPIX_C_FLOAT16, torch.float16, m.MPIX_ORDER_CHAIN)):
         esz = torch.tensor([], dtype=tdt).element_size()
         n = blk_bytes // esz
         stride = (blk_bytes + 4352) // esz
-        nsets = max(3, (3 << 30) // (9 * blk_bytes) + 1)
-        sets = [torch.empty(8 * stride, device="cuda", dtype=tdt).uniform_(-1, 1, generator=g) for _ in range(nsets)]
+        nsets = max(3, (3 << 30) // ((p + 1) * blk_bytes) + 1)
+        sets = [torch.empty(p * stride, device="cuda", dtype=tdt).uniform_(-1, 1, generator=g) for _ in range(nsets)]
         outs = [torch.empty(n, device="cuda", dtype=tdt) for _ in range(nsets)]
-        ops = [[s.data_ptr() + j * stride * esz for j in range(8)] for s in sets]
+        ops = [[s.data_ptr() + j * stride * esz for j in range(p)] for s in sets]
         torch.cuda.synchronize()
 
         def launch(i):
@@ -70,7 +73,7 @@ def main():
             e1.synchronize()
             per.append(e0.elapsed_time(e1) * 1e3 / 20)
         med = statistics.median(per)
-        print(f"{tag} {name}: median {med:.2f} us = {9 * blk_bytes / (med * 1e-6) / 8e12:.4f} of 8 TB/s "
+        print(f"{tag} {name}: median {med:.2f} us = {(p + 1) * blk_bytes / (med * 1e-6) / 8e12:.4f} of 8 TB/s "
               f"(rounds {', '.join(f'{x:.1f}' for x in per)}) output sha256 {digest}", flush=True)
         del sets, outs
         torch.cuda.empty_cache()
