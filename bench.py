@@ -50,7 +50,11 @@ Extra fields (rank 0):
   cpu_baseline  the oracle's C loop (reference algorithm, gcc -O2) on this box's host
                 cores, one pinned thread per physical core (as many as the job's CPU
                 quota allows; every physical core as a secondary, throttled figure),
-                NUMA-local operands, a bounded sample (rank 0, N = 1 only); per socket.
+                NUMA-local operands, a bounded sample, per socket; rank 0 at every N,
+                after the GPU work, the other ranks parked on a blocking store read.
+  call_distribution  rank 0's K timed calls one by one (median, p10 / p90,
+                mean, min / max; per-call clock stamps in the C loop), and the
+                call split into kernel + fixed cost.
 """
 from __future__ import annotations
 
@@ -144,22 +148,42 @@ def cpu_standin(args) -> None:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
 
-    own = []
-    dt = time_steps(step, args.steps, args.warmup, lambda: None, barrier, max_over_ranks, own)
-    rows = gather_rows([float(rank), own[0]], world, dist, "cpu")
+    own, calls = [], []
+    dt = time_steps(step, args.steps, args.warmup, lambda: None, barrier, max_over_ranks, own, calls)
+    alg = 3 * a.nbytes
+    cstats = call_stats(calls, alg)
+    rows = gather_rows([float(rank), own[0], cstats["median_us"]], world, dist, "cpu")
+    out = {"metric": METRIC, "value": None, "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
+           "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 4),
+           "per_rank": [{"rank": int(r[0]), "seconds": round(r[1], 6),
+                         "ms_per_step": round(r[1] / args.steps * 1e3, 4), "call_median_us": r[2]} for r in rows],
+           "call_distribution": dict(cstats, source="perf_counter after each stand-in step (rank 0)"),
+           "data": "cpu stand-in (test only, not a measurement)"}
+    # the collectives block's row format (bench_coll.coll_row) over the
+    # stand-in's per-rank times, as the GPU run reports configs 4 and 5
+    import bench_coll
+    per = [r[1] / args.steps for r in rows]
+    out["collectives"] = {"stand_in": True,
+                          "config4_allreduce_fp32_sum_256MiB": {"rccl": bench_coll.coll_row(per, world, alg, "allreduce")},
+                          "config5_reduce_scatter_block_fp16_sum_1GiB": {
+                              "rccl": bench_coll.coll_row(per, world, alg, "reduce_scatter")}}
+    if rank == 0 and not args.no_cpu_baseline:
+        # the real baseline routine on a small sample
+        out["cpu_baseline"] = cpu_baseline(args, 1 << 16, 3 * (1 << 18))
+        out["cpu_baseline"]["ranks_parked"] = world - 1
+    if not args.no_cpu_baseline:
+        park_until_rank0(world > 1, world, rank, dist, "bench_cpu_baseline_done")
     if rank == 0:
-        print(json.dumps({"metric": METRIC, "value": None, "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
-                          "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 4),
-                          "per_rank": [{"rank": int(r[0]), "seconds": round(r[1], 6),
-                                        "ms_per_step": round(r[1] / args.steps * 1e3, 4)} for r in rows],
-                          "data": "cpu stand-in (test only, not a measurement)"}), flush=True)
+        print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
 
 
-def time_steps(step, k: int, w: int, sync, barrier, max_over_ranks, own: list | None = None) -> float:
+def time_steps(step, k: int, w: int, sync, barrier, max_over_ranks, own: list | None = None,
+               calls: list | None = None) -> float:
     """W untimed steps, then exactly K steps bracketed by barrier + device sync; max over ranks.
-    `own`, if given, receives this rank's own seconds (for the per-rank report).
+    `own`, if given, receives this rank's own seconds (for the per-rank report);
+    `calls` each timed step's own duration (a clock read after every step).
     Python's cyclic garbage collector is held off while the K steps run, as
     timeit does: a full collection over torch's objects can take milliseconds,
     which the Python-stepped loops would otherwise count as a step."""
@@ -170,9 +194,15 @@ def time_steps(step, k: int, w: int, sync, barrier, max_over_ranks, own: list | 
     sync()
     gc_on = gc.isenabled()
     gc.disable()
+    stamps = [] if calls is not None else None
     t0 = time.perf_counter()
-    for i in range(k):
-        step(w + i)
+    if stamps is None:
+        for i in range(k):
+            step(w + i)
+    else:
+        for i in range(k):
+            step(w + i)
+            stamps.append(time.perf_counter())
     sync()
     t1 = time.perf_counter()
     if gc_on:
@@ -180,6 +210,8 @@ def time_steps(step, k: int, w: int, sync, barrier, max_over_ranks, own: list | 
     barrier()
     if own is not None:
         own.append(t1 - t0)
+    if calls is not None:
+        calls.extend(b - a for a, b in zip([t0] + stamps[:-1], stamps))
     return max_over_ranks(t1 - t0)
 
 
@@ -220,26 +252,70 @@ def run_collectives_child(rank: int, world: int, local: int, barrier, timeout: f
     return {}
 
 
-def time_loop(run, k: int, w: int, sync, barrier, max_over_ranks, own: list | None = None) -> float:
-    """time_steps for a C loop: run(start, n) makes steps start .. start + n - 1
-    back to back; W untimed steps, then exactly K timed ones between barrier +
-    device sync, max over ranks."""
+def time_loop(run, k: int, w: int, sync, barrier, max_over_ranks, own: list | None = None,
+              calls: list | None = None) -> float:
+    """time_steps for a C loop: run(start, n[, stamps]) makes steps start ..
+    start + n - 1 back to back; W untimed steps, then exactly K timed ones
+    between barrier + device sync, max over ranks.  `calls`, if given, receives
+    the K timed calls' own durations (seconds), from the loop's per-call clock
+    stamps."""
     run(0, w)
     sync()
     barrier()
     sync()
+    stamps = None
+    if calls is not None:
+        import numpy as np
+        stamps = np.zeros(k + 1, np.int64)
     t0 = time.perf_counter()
-    run(w, k)
+    if stamps is None:
+        run(w, k)
+    else:
+        run(w, k, stamps)
     sync()
     t1 = time.perf_counter()
     barrier()
     if own is not None:
         own.append(t1 - t0)
+    if calls is not None:
+        calls.extend((np.diff(stamps) * 1e-9).tolist())
     return max_over_ranks(t1 - t0)
 
 
+def call_stats(calls: list, alg_bytes: int) -> dict:
+    """The timed calls' own distribution: median, p10 / p90,
+    mean, min / max in us, and the median call's fraction of the HBM peak."""
+    v = sorted(calls)
+    n = len(v)
+    med = v[n // 2]
+    return {"calls": n, "median_us": round(med * 1e6, 2), "p10_us": round(v[n // 10] * 1e6, 2),
+            "p90_us": round(v[min(n - 1, (n * 9) // 10)] * 1e6, 2), "mean_us": round(sum(v) / n * 1e6, 2),
+            "min_us": round(v[0] * 1e6, 2), "max_us": round(v[-1] * 1e6, 2),
+            "frac_of_hbm_peak_at_median": round(alg_bytes / med / HBM_PEAK_BPS, 4)}
+
+
+def park_until_rank0(use_pg: bool, world: int, rank: int, dist, key: str, timeout_s: float = 900.0):
+    """Ranks other than 0 wait for rank 0's `key` on the process group's store
+    (a blocking socket read, no spin), so rank 0's CPU work runs beside idle
+    ranks; rank 0 sets it.  Falls back to a barrier if the store is unavailable."""
+    if not use_pg or world == 1:
+        return
+    import datetime
+    try:
+        store = dist.distributed_c10d._get_default_store()
+    except Exception:       # noqa: BLE001
+        store = None
+    if store is None:
+        dist.barrier()
+        return
+    if rank == 0:
+        store.set(key, "1")
+    else:
+        store.wait([key], datetime.timedelta(seconds=timeout_s))
+
+
 def sync_loops(m, lib, reduce_local, ptrs, count, k: int, w: int, sync, barrier, max_over_ranks,
-               own: list | None = None, c_loop=None):
+               own: list | None = None, c_loop=None, calls: list | None = None):
     """The headline loop (NPAIRS pairs rotated: every call after the first
     NPAIRS repeats its kernel arguments, which the direct dispatch's kernarg
     cache then holds) and the same loop with fresh arguments on every call: the
@@ -250,7 +326,8 @@ def sync_loops(m, lib, reduce_local, ptrs, count, k: int, w: int, sync, barrier,
     back to back in C, as a C caller issues them; the same loop stepped from
     Python, one compiled call per step, is timed last (`dt_py`).
     Returns seconds of each, the kernarg writes per timed fresh call, a
-    one-call step function and dt_py (None without c_loop)."""
+    one-call step function and dt_py (None without c_loop); `calls` receives
+    the headline loop's per-call durations."""
     dt_f32, op_sum = m.MPI_FLOAT, m.MPI_SUM
     call_args = tuple((pin, pio, count, dt_f32, op_sum) for pin, pio in ptrs)
     fresh_args = tuple((pin + o, pio + o, count, dt_f32, op_sum) for o in range(0, SLACK, 256) for pin, pio in ptrs)
@@ -266,20 +343,20 @@ def sync_loops(m, lib, reduce_local, ptrs, count, k: int, w: int, sync, barrier,
             raise RuntimeError(m.error_string(rc))
 
     def runner(sets):
-        def run(start, n):
-            rc = c_loop(sets, start, n)
+        def run(start, n, stamps=None):
+            rc = c_loop(sets, start, n, stamps)
             if rc:
                 raise RuntimeError(m.error_string(rc))
         return run
     dt_py = None
     if c_loop is not None:
-        dt = time_loop(runner(call_args), k, w, sync, barrier, max_over_ranks, own)
+        dt = time_loop(runner(call_args), k, w, sync, barrier, max_over_ranks, own, calls)
         kw0 = lib.MPIR_Hip_direct_kernarg_writes()
         dtf = time_loop(runner(fresh_args), k, w, sync, barrier, max_over_ranks, own)
         writes = (lib.MPIR_Hip_direct_kernarg_writes() - kw0) / (k + w)
         dt_py = time_steps(step, k, w, sync, barrier, max_over_ranks)
     else:
-        dt = time_steps(step, k, w, sync, barrier, max_over_ranks, own)
+        dt = time_steps(step, k, w, sync, barrier, max_over_ranks, own, calls)
         kw0 = lib.MPIR_Hip_direct_kernarg_writes()
         dtf = time_steps(fstep, k, w, sync, barrier, max_over_ranks, own)
         writes = (lib.MPIR_Hip_direct_kernarg_writes() - kw0) / (k + w)
@@ -644,7 +721,7 @@ def cpu_baseline(args, count: int, alg_bytes: int) -> dict:
     res = {"unit": "GiB/s", "kind": "port", "cores": len(cores)}
     res.update(g)
     res["sample"] = (f"{len(cores)} threads, one pinned per physical core (dealt over the sockets), {iters} calls each "
-                     f"of MPI_SUM MPI_FLOAT count {per} on its own first-touched 256 MiB (inbuf, inoutbuf) pair; "
+                     f"of MPI_SUM MPI_FLOAT count {per} on its own first-touched {per * 4 / MIB:g} MiB (inbuf, inoutbuf) pair; "
                      f"oracle/op_oracle.c SUM loop, gcc -O2 (MPICH's default build); aggregate = algorithmic bytes of "
                      f"all threads / slowest thread")
     res["machine"] = {"physical_cores": len(machine), "cgroup_cpu_quota": quota, "lscpu": lscpu_topology()}
@@ -770,16 +847,19 @@ def main():
         binding = "C loop of the compiled binding (csrc/py/fastcall.c reduce_local_loop)"
     except ImportError:     # extension not built: the same C entry point through ctypes
         reduce_local, c_loop, binding = lib.MPI_Reduce_local, None, "ctypes"
-    own = []
+    own, calls = [], []
     d_before = lib.MPIR_Hip_direct_dispatches()
     dt, dt_fresh, fresh_writes, step, dt_py = sync_loops(m, lib, reduce_local, ptrs, count, args.steps,
-                                                         args.warmup, sync, barrier, max_over_ranks, own, c_loop)
+                                                         args.warmup, sync, barrier, max_over_ranks, own, c_loop,
+                                                         calls)
+    cstats = call_stats(calls, alg_bytes)
     direct_share = (lib.MPIR_Hip_direct_dispatches() - d_before) / ((3 if c_loop else 2) * (args.steps + args.warmup))
     value = alg_bytes * args.steps * world / dt / GIB
     # each rank's own figures beside the max-over-ranks `value`: a lagging GPU,
     # or a rank whose calls left the direct path, shows here
     rows = gather_rows([float(rank), float(dev), own[0], own[1], float(lib.MPIR_Hip_direct_state(dev)),
-                        direct_share], world, dist, "cpu" if pg_backend == "gloo" else "cuda")
+                        direct_share, cstats["median_us"], cstats["p10_us"], cstats["p90_us"]], world, dist,
+                       "cpu" if pg_backend == "gloo" else "cuda")
 
     def rate(seconds):
         v = alg_bytes * args.steps * world / seconds / GIB
@@ -829,7 +909,11 @@ def main():
                       "GiBps": round(alg_bytes * args.steps / r[2] / GIB, 1),
                       "frac_of_hbm_peak": round(alg_bytes * args.steps / r[2] / HBM_PEAK_BPS, 4),
                       "fresh_args_seconds": round(r[3], 6), "direct_state": int(r[4]),
-                      "direct_share": round(r[5], 4)} for r in rows],
+                      "direct_share": round(r[5], 4),
+                      "call_median_us": r[6], "call_p10_p90_us": [r[7], r[8]]} for r in rows],
+        # rank 0's K timed calls, each on its own (clock stamps in the C loop)
+        "call_distribution": dict(cstats, source="CLOCK_MONOTONIC after each call of the timed C loop (rank 0)"
+                                  if c_loop else "perf_counter after each step of the timed loop (rank 0)"),
     }
 
     variants = {"fresh_args": dict(rate(dt_fresh), kernarg_writes_per_call=round(fresh_writes, 3),
@@ -904,6 +988,15 @@ def main():
                                   "mean_launch_us_hip_events": round(ev_mean_us, 2),
                                   "frac": round(alg_bytes / (ev_mean_us * 1e-6) / HBM_PEAK_BPS, 4)},
         }
+        # the synchronous call = kernel + a fixed cost (dispatch, completion,
+        # host): what the kernel must reach for the call to reach 0.80
+        call_mean_us = dt / args.steps * 1e6
+        fixed = call_mean_us - mean_us
+        out["call_distribution"]["decomposition"] = {
+            "call_mean_us": round(call_mean_us, 2), "kernel_mean_us": round(mean_us, 2),
+            "fixed_us": round(fixed, 2), "call_median_minus_kernel_median_us": round(
+                cstats["median_us"] - us_sorted[len(us_sorted) // 2], 2),
+            "kernel_us_for_call_at_0.80": round(alg_bytes / (0.8 * HBM_PEAK_BPS) * 1e6 - fixed, 2)}
 
         # ---- configs 2 and 3 (kernel time per synchronous call, same method)
         out["config3_sweep"] = config3_sweep(m, lib, pairs, nbytes, s)
@@ -968,8 +1061,14 @@ def main():
         if rank == 0:
             out["collectives"] = coll
 
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    # the CPU baseline on rank 0 at every N, after the GPU work, the other
+    # ranks parked on a blocking store read (no spinning core beside it)
+    if rank == 0 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args, count, alg_bytes)
+        if world > 1:
+            out["cpu_baseline"]["ranks_parked"] = world - 1
+    if not args.no_cpu_baseline:
+        park_until_rank0(use_pg, world, rank, dist, "bench_cpu_baseline_done")
     if rank == 0:
         print(json.dumps(out), flush=True)
     if use_pg:

@@ -21,7 +21,10 @@ unique id exchanged over a TCPStore on 127.0.0.1), then
      (recvcount 2^29 / N).  Both algorithms (RCCL, reference order); K timed
      calls between a barrier and a device sync, max over ranks.
 Reports bus bandwidth the RCCL-tests way: allreduce 2(N-1)/N * bytes / t,
-reduce-scatter (N-1)/N * sendbytes / t.
+reduce-scatter (N-1)/N * sendbytes / t, every rank's own time beside the
+max-over-ranks one, and the bus bandwidth as a fraction of the xGMI roofline
+(coll_row below): 7 links x 153 GB/s per GPU on a fully connected 8-GPU node
+(SURVEY.md:254 and :399), and of the N - 1 links an N-rank collective can use.
 """
 from __future__ import annotations
 
@@ -36,6 +39,30 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "mpich-pip_amd"))
 sys.path.insert(0, ROOT)
+
+
+XGMI_LINK_GBPS = 153.0        # one xGMI link, GB/s per direction (SURVEY.md:254)
+XGMI_LINKS = 7                # per GPU, fully connected 8-GPU node
+
+
+def coll_row(per_rank_s: list, world: int, nbytes: int, kind: str) -> dict:
+    """One timed collective: per-rank seconds per call -> its report row.
+    kind "allreduce": busbw = 2(N-1)/N * bytes / t; "reduce_scatter": (N-1)/N
+    * sendbytes / t (RCCL-tests).  t is the slowest rank's.  frac_of_xgmi =
+    busbw / (7 x 153 GB/s), the per-GPU xGMI peak of the 8-GPU node;
+    frac_of_links_in_use = busbw / ((N-1) x 153 GB/s), the links an N-rank
+    collective can drive (one to each peer)."""
+    t = max(per_rank_s)
+    factor = 2 * (world - 1) / world if kind == "allreduce" else (world - 1) / world
+    bus = factor * nbytes / t / 1e9
+    row = {"ms": round(t * 1e3, 3), "per_rank_ms": [round(x * 1e3, 3) for x in per_rank_s],
+           "busbw_GBps": round(bus, 1),
+           "frac_of_xgmi": round(bus / (XGMI_LINKS * XGMI_LINK_GBPS), 4),
+           "frac_of_links_in_use": round(bus / (max(1, world - 1) * XGMI_LINK_GBPS), 4) if world > 1 else None,
+           "xgmi_peak": f"{XGMI_LINKS} links x {XGMI_LINK_GBPS:g} GB/s per GPU (SURVEY.md:254)"}
+    if kind == "allreduce":
+        row["algbw_GBps"] = round(nbytes / t / 1e9, 1)
+    return row
 
 
 def _bitrev(n: int, bits: int) -> int:
@@ -149,10 +176,12 @@ def main():
         torch.cuda.synchronize()
         assert m.allreduce(m.MPI_IN_PLACE, scratch.data_ptr(), 1, m.MPI_DOUBLE, SUM, C, RCCL) == 0
 
-    def max_over_ranks(x):
-        t = torch.tensor([x], dtype=torch.float64, device="cuda")
-        assert m.allreduce(m.MPI_IN_PLACE, t.data_ptr(), 1, m.MPI_DOUBLE, MAX, C, RCCL) == 0
-        return float(t.item())
+    def per_rank(x):
+        """every rank's x, in rank order (a SUM of one-hot rows)"""
+        t = torch.zeros(world, dtype=torch.float64, device="cuda")
+        t[rank] = x
+        assert m.allreduce(m.MPI_IN_PLACE, t.data_ptr(), world, m.MPI_DOUBLE, SUM, C, RCCL) == 0
+        return t.cpu().tolist()
 
     out = {"n_ranks": world}
 
@@ -245,7 +274,7 @@ def main():
             fn()
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
-        return max_over_ranks(dt) / args.steps
+        return [x / args.steps for x in per_rank(dt)]
 
     count = args.ar_mib * (1 << 20) // 4
     a = torch.rand(count, device="cuda") * 2 - 1
@@ -262,10 +291,7 @@ def main():
 
     res = {}
     for name, alg in (("rccl", RCCL), ("reference_order", REF)):
-        t = timed(lambda: ar(alg))
-        nbytes = count * 4
-        res[name] = {"ms": round(t * 1e3, 3), "algbw_GBps": round(nbytes / t / 1e9, 1),
-                     "busbw_GBps": round(2 * (world - 1) / world * nbytes / t / 1e9, 1)}
+        res[name] = coll_row(timed(lambda: ar(alg)), world, count * 4, "allreduce")
     out["config4_allreduce_fp32_sum_256MiB"] = res
     del a, b
     torch.cuda.empty_cache()
@@ -276,9 +302,7 @@ def main():
     hr_ = torch.empty(rc_, dtype=torch.float16, device="cuda")
     res = {}
     for name, alg in (("rccl", RCCL), ("reference_order", REF)):
-        t = timed(lambda: rs(alg))
-        sb = rc_ * world * 2
-        res[name] = {"ms": round(t * 1e3, 3), "busbw_GBps": round((world - 1) / world * sb / t / 1e9, 1)}
+        res[name] = coll_row(timed(lambda: rs(alg)), world, rc_ * world * 2, "reduce_scatter")
     out["config5_reduce_scatter_block_fp16_sum_1GiB"] = res
     m.comm_free(C)
     if rank == 0:

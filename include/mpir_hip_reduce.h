@@ -167,6 +167,19 @@ uint32_t MPIR_Hip_direct_test_write_delay_us(uint32_t us);
 void MPIR_Hip_direct_test_fail_probe(void);
 int MPIR_Hip_thread_contexts(void);
 
+/* Ranks of this job on this node, for sizing the host combine's threads: the
+ * node's CPUs are shared by every local rank, and all of them reach the
+ * combine of a host-buffer MPI_Allreduce together.  Inside libmpi the op layer
+ * passes MPICH's node communicator size (mpich_glue.c) before its first
+ * combine; otherwise MPI_LOCALNRANKS / MPIR_PIP_SIZE / LOCAL_WORLD_SIZE /
+ * OMPI_COMM_WORLD_LOCAL_SIZE, else 1.  Takes effect if called before the first
+ * host combine sizes the pool; returns the previous value (0 = unset). */
+int MPIR_Hip_set_local_ranks(int n);
+/* Threads one host combine uses, the caller included (1 = the caller alone):
+ * this rank's share of the node's CPUs, at most 16, or
+ * MPIR_CVAR_REDUCE_LOCAL_STAGE_THREADS.  Sizes the pool without starting it. */
+int MPIR_Hip_host_threads(void);
+
 #ifdef __cplusplus
 }
 #endif

@@ -758,9 +758,12 @@ int direct_reduce(int dev, int op, int elem, const ReducePlan &p, int *rc) {
             *d.hdp = 1u;
         }
         // a checked grid spans every XCD (kMinCheckedGroups): then each XCD's
-        // L2 holds the fresh line, or none, when a later hit runs unchecked
+        // L2 holds the fresh line, or none, when a later hit runs unchecked.
+        // Read-back mode pads its misses too: their dispatch marks
+        // the entry verified as well, and the unchecked kernels' extra
+        // workgroups start past the region and exit
         publish_packet(q, idx, checked && !rb ? ko_checked : ko, slot, sig, kThreads,
-                       checked && !rb && groups < kMinCheckedGroups ? kMinCheckedGroups : groups);
+                       checked && groups < kMinCheckedGroups ? kMinCheckedGroups : groups);
         if (prof) th1 = sys_ts();
         hsa_signal_store_screlease(q->doorbell_signal, idx);
         if (late) {

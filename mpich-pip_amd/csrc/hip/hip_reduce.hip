@@ -22,6 +22,7 @@
 #include <vector>
 
 #include <hsa/hsa.h>
+#include <hsa/hsa_ext_amd.h>
 
 #include "mpir_hip_reduce.h"
 #include "kernel_table.hpp"
@@ -328,36 +329,76 @@ class CopyPool {
     uint64_t gen_ = 0;
 };
 
-// CPUs this process may run on: its affinity mask, capped by a cgroup v2 CPU
-// quota (cpu.max "quota period"), as a container or batch job sets it.
-int usable_cpus() {
-    cpu_set_t set;
-    int n = sched_getaffinity(0, sizeof set, &set) == 0 ? CPU_COUNT(&set) : 1;
+// Ranks of this job on this node (>= 1).  Every rank of a host-buffer
+// MPI_Allreduce reaches its combine at the same moment, so the node's CPUs are
+// shared by all of them.  Sources, in order: MPIR_Hip_set_local_ranks() (inside
+// libmpi the glue passes MPICH's node communicator size, mpich_glue.c), then
+// the launcher's environment -- MPI_LOCALNRANKS (Hydra, pmip_cb.c:658-662),
+// MPIR_PIP_SIZE (this repo's mpiexec: one node), LOCAL_WORLD_SIZE (torchrun),
+// OMPI_COMM_WORLD_LOCAL_SIZE (Open MPI's launcher); none: 1.
+std::atomic<int> g_local_ranks{0};
+int local_ranks() {
+    const int set = g_local_ranks.load(std::memory_order_relaxed);
+    if (set > 0) return set;
+    static const int env = [] {
+        for (const char *k : {"MPI_LOCALNRANKS", "MPIR_PIP_SIZE", "LOCAL_WORLD_SIZE", "OMPI_COMM_WORLD_LOCAL_SIZE"})
+            if (const char *e = getenv(k)) {
+                const int n = atoi(e);
+                if (n >= 1 && n <= (1 << 20)) return n;
+            }
+        return 1;
+    }();
+    return env;
+}
+
+// Host-combine threads for one rank, from the CPUs the node's L local ranks
+// share (the reference's combine is one thread per rank,
+// opsum.c:21-76):
+//   * affinity: a mask of m of the node's c online CPUs.  Ranks bound to
+//     disjoint sets (L * m <= c) each own their mask; unbound ranks (m = c)
+//     share it L ways; in between (e.g. --bind-to socket) ceil(L * m / c)
+//     ranks share each mask;
+//   * cgroup quota q (cpu.max): the job's or container's, shared by all L.
+// The share is at most 16 (the host combine's measured scaling: 256 MiB fp32
+// SUM, 16-CPU quota, 131-136 GiB/s on 4 threads, 259-299 on 16;
+// profiles/archive/r02/host_threads_ab.log).  No floor: with at most one CPU
+// per rank the caller combines alone and the library starts no thread, as
+// MPICH's loop starts none (8 unbound ranks on this job's 16-CPU quota: one
+// worker each beside the caller).  Copies (bounce path, mixed-residency slots)
+// keep to at most 4 parts, which already outrun a PCIe upload.
+// MPIR_CVAR_REDUCE_LOCAL_STAGE_THREADS sets both (1 = the caller alone).
+// (pool_threads() sizes a pool without creating one: the floating pool's
+// threads start only when a copy or a combine off the operands' node needs
+// them, never beside a NUMA node's pool that does the work; the size is fixed
+// at the first call, so MPIR_Hip_set_local_ranks() acts before the first host
+// combine)
+int online_cpus() {
+    const long n = sysconf(_SC_NPROCESSORS_ONLN);
+    return n >= 1 ? (int)n : 1;
+}
+int cgroup_quota_cpus() {
+    int q = 0;
     if (FILE *f = fopen("/sys/fs/cgroup/cpu.max", "r")) {
         char quota[32];
         long period = 0;
         if (fscanf(f, "%31s %ld", quota, &period) == 2 && strcmp(quota, "max") != 0 && period > 0) {
-            const long q = (atol(quota) + period - 1) / period;
-            if (q >= 1 && q < n) n = (int)q;
+            const long v = (atol(quota) + period - 1) / period;
+            if (v >= 1 && v < (1L << 20)) q = (int)v;
         }
         fclose(f);
     }
-    return n;
+    return q;
 }
-
-// Default pool size: the usable CPUs (affinity mask and cgroup quota), at most
-// 16, for the host combine of large both-host operands, which is memory-bound
-// and scales with threads (256 MiB fp32 SUM on the MI355X host, 16-CPU quota:
-// 131-136 GiB/s on 4 threads, 259-299 on 16;
-// profiles/archive/r02/host_threads_ab.log).  No floor: a rank bound to one
-// CPU (mpiexec --bind-to core) combines on the calling thread alone and the
-// library starts no thread, as MPICH's loop starts none; two CPUs give one
-// worker beside the caller.  Copies (bounce path, mixed-residency slots) keep
-// to at most 4 parts, which already outrun a PCIe upload.
-// MPIR_CVAR_REDUCE_LOCAL_STAGE_THREADS sets both (1 = the caller alone).
-// (pool_threads() sizes a pool without creating one: the floating pool's
-// threads start only when a copy or a combine off the operands' node needs
-// them, never beside a NUMA node's pool that does the work)
+int share_threads(int mask, int online, int quota, int L) {
+    if (L < 1) L = 1;
+    if (mask < 1) mask = 1;
+    if (online < mask) online = mask;
+    int sharers = (int)(((long)L * mask + online - 1) / online);
+    sharers = std::max(1, std::min(L, sharers));
+    int n = mask / sharers;
+    if (quota > 0) n = std::min(n, quota / L);
+    return std::max(1, std::min(16, n));
+}
 const char *stage_threads_env() {
     static const char *e = getenv("MPIR_CVAR_REDUCE_LOCAL_STAGE_THREADS");
     return e;
@@ -365,8 +406,13 @@ const char *stage_threads_env() {
 int pool_threads() {
     static const int n = [] {
         const char *e = stage_threads_env();
-        const int v = e ? atoi(e) : std::min(16, usable_cpus());
-        return v < 1 || v > 64 ? (e ? 4 : 1) : v;
+        if (e) {
+            const int v = atoi(e);
+            return v < 1 || v > 64 ? 4 : v;
+        }
+        cpu_set_t set;
+        const int mask = sched_getaffinity(0, sizeof set, &set) == 0 ? CPU_COUNT(&set) : 1;
+        return share_threads(mask, online_cpus(), cgroup_quota_cpus(), local_ranks());
     }();
     return n;
 }
@@ -589,10 +635,9 @@ bool gpu_runtime_started() {
     return true;
 }
 
-// Device memory (hipMalloc, managed) is combined in place; host memory
-// (pageable or pinned) takes the host combine, the pinned slot or staging.
-Loc classify(const void *p, int *dev) {
-    if (!gpu_runtime_started()) return LOC_HOST;
+// HIP's view of a pointer (100-165 ns a query once HIP is up:
+// profiles/r05/classify_cost.log)
+Loc classify_hip(const void *p, int *dev) {
     hipPointerAttribute_t at;
     hipError_t e = hipPointerGetAttributes(&at, p);
     if (e != hipSuccess) {
@@ -606,6 +651,98 @@ Loc classify(const void *p, int *dev) {
     if (at.type != hipMemoryTypeHost) return LOC_HOST;
     *dev = at.device;       // the device whose context allocated (registered) it
     return LOC_PINNED;
+}
+
+// HIP device ordinal of each HSA GPU agent, matched by PCI domain, bus and
+// device (HIP_VISIBLE_DEVICES may hide and renumber agents HSA still lists).
+// Empty when any visible device matches no agent or more than one (e.g. a
+// partition mode sharing one BDF): the HSA query then answers nothing.
+struct AgentMap {
+    int n = 0;
+    uint64_t handle[kMaxDev];
+    int dev[kMaxDev];
+};
+const AgentMap &agent_map() {
+    static const AgentMap m = [] {
+        AgentMap am;
+        struct Gpu { uint64_t handle; uint32_t bdf, domain; };
+        std::vector<Gpu> gpus;
+        (void)hsa_iterate_agents([](hsa_agent_t a, void *v) {
+            hsa_device_type_t t;
+            if (hsa_agent_get_info(a, HSA_AGENT_INFO_DEVICE, &t) != HSA_STATUS_SUCCESS || t != HSA_DEVICE_TYPE_GPU)
+                return HSA_STATUS_SUCCESS;
+            Gpu g{a.handle, 0, 0};
+            if (hsa_agent_get_info(a, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_BDFID, &g.bdf) != HSA_STATUS_SUCCESS ||
+                hsa_agent_get_info(a, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_DOMAIN, &g.domain) != HSA_STATUS_SUCCESS)
+                return HSA_STATUS_SUCCESS;
+            static_cast<std::vector<Gpu> *>(v)->push_back(g);
+            return HSA_STATUS_SUCCESS;
+        }, &gpus);
+        int ndev = 0;
+        if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0 || ndev > kMaxDev) {
+            (void)hipGetLastError();
+            return am;
+        }
+        for (int d = 0; d < ndev; ++d) {
+            int dom = 0, bus = 0, slot = 0;
+            if (hipDeviceGetAttribute(&dom, hipDeviceAttributePciDomainID, d) != hipSuccess ||
+                hipDeviceGetAttribute(&bus, hipDeviceAttributePciBusId, d) != hipSuccess ||
+                hipDeviceGetAttribute(&slot, hipDeviceAttributePciDeviceId, d) != hipSuccess) {
+                (void)hipGetLastError();
+                return AgentMap();
+            }
+            int hits = 0;
+            for (const Gpu &g : gpus)
+                if (g.domain == (uint32_t)dom && ((g.bdf >> 8) & 0xff) == (uint32_t)bus &&
+                    ((g.bdf >> 3) & 0x1f) == (uint32_t)slot) {
+                    am.handle[am.n] = g.handle;
+                    am.dev[am.n] = d;
+                    ++hits;
+                }
+            if (hits != 1) return AgentMap();
+            ++am.n;
+        }
+        return am;
+    }();
+    return m;
+}
+
+int agent_device(hsa_agent_t a) {
+    const AgentMap &m = agent_map();
+    for (int i = 0; i < m.n; ++i)
+        if (m.handle[i] == a.handle) return m.dev[i];
+    return -1;
+}
+
+// Device memory (hipMalloc, stream-ordered pools, VMM mappings, IPC imports,
+// managed) is combined in place; host memory (pageable or pinned) takes the
+// host combine, the pinned slot or staging.  One HSA pointer query (24-66 ns
+// against HIP's 100-165, profiles/r05/classify_cost.log) answers for memory HSA
+// knows as a GPU's -- allocations of its pools (HSA), its virtual-memory
+// mappings (HSA_VMEM: stream-ordered pools, hipMemCreate + hipMemMap) and IPC imports
+// (hsa_ext_amd.h:2344-2372) -- and for memory it does not know at all (UNKNOWN),
+// which is host memory: pageable, or registered with hipHostRegister (HIP
+// registers without HSA's lock, so HSA reports it UNKNOWN; it is combined as
+// pageable memory, as MPICH itself treats a registered host buffer -- read in
+// place, no stream ordering).  Every other answer -- host pools (hipHostMalloc:
+// pinned, whose owning device orders the caller's null-stream work before the
+// read), managed memory (RESERVED_ADDR, no owner), graphics interop -- asks HIP.
+Loc classify(const void *p, int *dev) {
+    if (!gpu_runtime_started()) return LOC_HOST;
+    hsa_amd_pointer_info_t info;
+    info.size = sizeof info;
+    if (hsa_amd_pointer_info(p, &info, nullptr, nullptr, nullptr) == HSA_STATUS_SUCCESS) {
+        if (info.type == HSA_EXT_POINTER_TYPE_UNKNOWN) return LOC_HOST;
+        if (info.type == HSA_EXT_POINTER_TYPE_HSA || info.type == HSA_EXT_POINTER_TYPE_HSA_VMEM ||
+            info.type == HSA_EXT_POINTER_TYPE_IPC) {
+            const int d = agent_device(info.agentOwner);
+            if (d >= 0) {
+                *dev = d;
+                return LOC_DEVICE;
+            }
+        }
+    }
+    return classify_hip(p, dev);
 }
 
 // devices visible to this process (0 on a CPU-only rank: host operands are
@@ -814,6 +951,12 @@ uint64_t MPIR_Hip_direct_kernarg_writes(void) { return direct_kernarg_writes(); 
 uint32_t MPIR_Hip_direct_test_write_delay_us(uint32_t us) { return direct_test_write_delay_us(us); }
 void MPIR_Hip_direct_test_fail_probe(void) { direct_test_fail_probe(); }
 
+int MPIR_Hip_set_local_ranks(int n) {
+    return g_local_ranks.exchange(n > 0 ? n : 0);
+}
+
+int MPIR_Hip_host_threads(void) { return pool_threads(); }
+
 int MPIR_Hip_thread_contexts(void) {
     std::lock_guard<std::mutex> lk(g_pool_mu);
     return g_ctx_created;
@@ -940,12 +1083,12 @@ int MPIR_Hip_reduce(const void *inbuf, void *inoutbuf, uint64_t count, int op, i
         int rc = MPIR_HIP_OK;
         if (lin == LOC_PINNED || lio == LOC_PINNED) {
             // the host operand is read (copied into the slot) before device_call's
-            // own null-stream check: order it first
-            int cur = 0;
-            HIPCHK(hipGetDevice(&cur));
-            if (cur != dev) HIPCHK(hipSetDevice(dev));
-            rc = order_after_null_stream();
-            if (cur != dev) (void)hipSetDevice(cur);
+            // own null-stream check: order it first, after the null stream of the
+            // device that owns the pinned buffer and of the device
+            // the kernel runs on
+            const int pdev = lin == LOC_PINNED ? din : dio;
+            rc = order_after_null_stream_of(pdev);
+            if (rc == MPIR_HIP_OK && pdev != dev) rc = order_after_null_stream_of(dev);
             if (rc != MPIR_HIP_OK) return rc;
         }
         rc = get_zc(dev, (size_t)bytes + 256, &slot);

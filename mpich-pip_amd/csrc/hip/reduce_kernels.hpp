@@ -645,10 +645,11 @@ __device__ __forceinline__ T fold_fast(const T (&v0)[P]) {
     return v[0];
 }
 
+// tile `blk` of the fused fold (TH threads, U vectors per lane per operand)
 template <class Op, class T, int P, bool TREE, int U, int TH>
-__global__ __launch_bounds__(TH) void k_combine_multi(MultiArgs a) {
+__device__ __forceinline__ void combine_multi_tile(const MultiArgs &a, uint64_t blk) {
     constexpr uint32_t tile = TH * U * 16;
-    const uint64_t base = (uint64_t)blockIdx.x * tile;
+    const uint64_t base = blk * tile;
     if (base < a.vbytes) {
         const uint64_t left = a.vbytes - base;
         const int nrec = (int)(left < tile ? left : tile);
@@ -684,6 +685,11 @@ __global__ __launch_bounds__(TH) void k_combine_multi(MultiArgs a) {
             store16(__builtin_bit_cast(u32x4, res), ro, wb + u * 1024, keep_tile(base, a.vbytes, a.keep));
         }
     }
+}
+
+template <class Op, class T, int P, bool TREE, int U, int TH>
+__global__ __launch_bounds__(TH) void k_combine_multi(MultiArgs a) {
+    combine_multi_tile<Op, T, P, TREE, U, TH>(a, blockIdx.x);
     if (blockIdx.x == 0) {
         const unsigned t = threadIdx.x;
         int64_t off = 0;

@@ -14,6 +14,9 @@
  *                            401-412; scan / exscan / reduce_scatter*), and
  *                            MPIR_Reduce_local's own reset / read
  *                            (reduce_local.c:51-59,107-117);
+ *   MPIR_Dropin_local_ranks() -> MPIR_Process.comm_world->node_comm->local_size,
+ *                            the ranks sharing this node's CPUs (sizes the
+ *                            host combine's threads; op_kernels.c);
  *   MPIR_DROPIN_CS_GLOBAL -> MPID_THREAD_CS_ENTER/EXIT(GLOBAL,
  *                            MPIR_THREAD_GLOBAL_ALLFUNC_MUTEX), the section
  *                            MPI_Reduce_local, MPI_Op_create, MPI_Op_free and
@@ -42,6 +45,19 @@ int *MPIR_Op_errno_ptr(void)
                                  MPIR_Per_thread, per_thread, &err);
     MPIR_Assert(err == 0);
     return &per_thread->op_errno;
+}
+
+/* Ranks of MPI_COMM_WORLD on this node: MPICH's node communicator
+ * (mpir_comm.h:148, built by MPIR_Comm_commit when the world is node-aware),
+ * else 0 (unknown: the library reads the launcher's environment).  The op
+ * layer hands it to MPIR_Hip_set_local_ranks() before its first combine, so the
+ * host combine's threads are this rank's share of the node's CPUs. */
+int MPIR_Dropin_local_ranks(void)
+{
+    MPIR_Comm *world = MPIR_Process.comm_world;
+    if (world && world->node_comm)
+        return world->node_comm->local_size;
+    return 0;
 }
 
 /* which: 0 = GLOBAL, 1 = HANDLE (enum in mpir_op_types.h, not included here:

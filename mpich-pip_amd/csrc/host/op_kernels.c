@@ -197,6 +197,30 @@ void MPIR_Op_report_hip_error(const char *opname, int hip_rc)
 
 /* ------------------------------------------------------------ kernels */
 
+#ifdef MPIR_DROPIN_IN_LIBMPI
+/* In libmpi: the node's rank count from MPICH's node communicator
+ * (mpich_glue.c), handed to the library once it is known, before the host
+ * combine sizes its threads (standalone, the library reads the launcher's
+ * environment itself). */
+int MPIR_Dropin_local_ranks(void);
+
+static inline void pass_local_ranks(void)
+{
+    static int passed;
+    if (__atomic_load_n(&passed, __ATOMIC_RELAXED))
+        return;
+    int n = MPIR_Dropin_local_ranks();
+    if (n > 0) {
+        MPIR_Hip_set_local_ranks(n);
+        __atomic_store_n(&passed, 1, __ATOMIC_RELAXED);
+    }
+}
+#else
+static inline void pass_local_ranks(void)
+{
+}
+#endif
+
 /* The body shared by every reference kernel: the datatype switch, then
  * either the combine (one GPU launch) or the `default:` branch that stores
  * MPI_ERR_OP ("**opundefined") in op_errno (e.g. opsum.c:59-73). */
@@ -213,6 +237,7 @@ static void op_apply(int opidx, const char *opname, void *invec, void *inoutvec,
     }
     if (len <= 0)       /* `for (i=0; i<len; i++)` runs zero times */
         return;
+    pass_local_ranks();
     rc = MPIR_Hip_reduce(invec, inoutvec, (uint64_t) len, opidx, elem, NULL, 1);
     if (rc != MPIR_HIP_OK)
         MPIR_Op_report_hip_error(opname, rc);

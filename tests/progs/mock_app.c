@@ -29,6 +29,7 @@ void mock_cs_counts(int *global, int *handle);
 int mock_progress_post(MPI_Op op);
 int mock_progress_poll(int max);
 int mock_avail_check(int *total_objects);
+void mock_set_node_ranks(int n);
 
 #define CHECK(c) do { if (!(c)) { fprintf(stderr, "FAIL %s:%d: %s\n", __FILE__, __LINE__, #c); return 1; } } while (0)
 
@@ -183,6 +184,17 @@ int main(void)
 {
     int in[3] = { 1, 2, 3 }, io[3] = { 5, 6, 7 }, created = 0, returned = 0, rc;
     MPI_Op op, handle;
+    int (*set_local_ranks)(int) = (int (*)(int)) dlsym(RTLD_DEFAULT, "MPIR_Hip_set_local_ranks");
+
+    /* before MPI_Init's world exists the op layer passes nothing; then the
+     * node communicator's size reaches the device layer at the next combine */
+    CHECK(set_local_ranks != NULL);
+    CHECK(mock_sched_reduce(in, io, 3, MPI_INT, MPI_SUM, NULL) == MPI_SUCCESS);
+    CHECK(set_local_ranks(0) == 0);
+    mock_set_node_ranks(3);
+    CHECK(mock_sched_reduce(in, io, 3, MPI_INT, MPI_SUM, NULL) == MPI_SUCCESS);
+    CHECK(set_local_ranks(3) == 3);
+    io[0] = 5, io[1] = 6, io[2] = 7;
 
     CHECK(MPI_Op_create(twice_plus, 0, &op) == MPI_SUCCESS);
     handle = op;

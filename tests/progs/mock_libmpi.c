@@ -46,6 +46,20 @@ MPID_Thread_mutex_t MPIR_THREAD_POBJ_HANDLE_MUTEX = { PTHREAD_RECURSIVE_MUTEX_IN
 #endif
 int mock_cs_global_enters, mock_cs_handle_enters;
 
+/* ---- "MPICH's" world and its node communicator (MPIR_Comm_commit) -------- */
+MPIR_Process_t MPIR_Process;
+static MPIR_Comm mock_world, mock_node;
+
+/* n > 0: a node-aware world whose node communicator holds n ranks; 0: none */
+__attribute__((visibility("default")))
+void mock_set_node_ranks(int n)
+{
+    mock_node.local_size = n;
+    mock_world.local_size = 2 * n;
+    mock_world.node_comm = n > 0 ? &mock_node : NULL;
+    MPIR_Process.comm_world = &mock_world;
+}
+
 /* MPI_Init_thread(MPI_THREAD_MULTIPLE) sets this (initthread.c) */
 __attribute__((visibility("default")))
 void mock_set_threaded(int on)

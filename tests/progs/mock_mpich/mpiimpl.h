@@ -85,6 +85,18 @@ extern int mock_cs_global_enters, mock_cs_handle_enters;
 #define MOCK_CS_EXIT_VCI(mx)     MOCK_UNLOCK(mx)
 #endif
 
+/* the communicator fields the glue reads (mpir_comm.h:134,148) and the
+ * process struct that holds the world (mpir_process.h:34-38) */
+typedef struct MPIR_Comm {
+    int local_size;
+    struct MPIR_Comm *node_comm;
+} MPIR_Comm;
+
+typedef struct {
+    MPIR_Comm *comm_world;
+} MPIR_Process_t;
+extern MPIR_Process_t MPIR_Process;
+
 #define MPID_THREAD_CS_ENTER(name, mutex) MOCK_CS_ENTER_##name(mutex)
 #define MPID_THREAD_CS_EXIT(name, mutex)  MOCK_CS_EXIT_##name(mutex)
 

@@ -32,15 +32,17 @@ def main():
     d0 = lib.MPIR_Hip_direct_dispatches()
     ok = True
     # profiled (twin queue: the failing probe runs inside the first call), then
-    # the calls' own queue; offsets give fresh arguments, repeats cache hits
+    # the calls' own queue; offsets give fresh arguments, repeats cache hits.
+    # Small counts (grids of 1-7 workgroups, padded to span every XCD on a
+    # miss, read-back mode included: ADVICE r4) fresh and repeated
     for prof in (1, 1, 1, 0, 0, 0, 0):
         lib.MPIR_Hip_direct_profile(prof)
-        for off in (0, 3, 0):
+        for cnt, off in ((n, 0), (n, 3), (n, 0), (3001, 0), (3001, 0), (77, 1), (77, 1), (4096 * 5, 2)):
             a = a0.clone()
             torch.cuda.synchronize()
-            rc = f(b.data_ptr() + 4 * off, a.data_ptr() + 4 * off, n, m.MPI_FLOAT, m.MPI_SUM)
+            rc = f(b.data_ptr() + 4 * off, a.data_ptr() + 4 * off, cnt, m.MPI_FLOAT, m.MPI_SUM)
             want = a0.clone()
-            want[off:off + n] += b[off:off + n]
+            want[off:off + cnt] += b[off:off + cnt]
             good = rc == 0 and bool(torch.equal(a, want))
             ok &= good
             out["calls"].append([prof, off, rc, good, int(lib.MPIR_Hip_direct_last_kernel_ns()) if prof else None])

@@ -1,0 +1,174 @@
+"""Every kind of buffer a caller can hand MPI_Reduce_local, classified by the
+HSA pointer query (hip_reduce.hip classify) and reduced
+bit-exact against the oracle.  The reference runs no query at all: its loop
+reads host memory (reduce_local.c:35-122, opsum.c:21-76).
+
+Kinds: hipMalloc, hipMallocAsync (stream-ordered pool: HSA_VMEM), VMM
+(hipMemCreate + hipMemAddressReserve + hipMemMap: HSA_VMEM), hipMallocManaged
+(RESERVED_ADDR: asks HIP), hipHostMalloc (HSA, CPU-owned: pinned),
+hipHostRegister'ed malloc memory (UNKNOWN to HSA: pageable path) and plain
+pageable memory.  Each kind is paired with a hipMalloc buffer in both roles
+(inbuf and inoutbuf) and with a buffer of its own kind; MPIR_Hip_is_device_ptr
+reports the class.
+"""
+import ctypes
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+N = (1 << 18) + 3                 # fp32 elements: ragged, ~1 MiB
+NB = N * 4
+
+
+class Loc(ctypes.Structure):
+    _fields_ = [("type", ctypes.c_int), ("id", ctypes.c_int)]
+
+
+class AllocFlags(ctypes.Structure):
+    _fields_ = [("compressionType", ctypes.c_ubyte), ("gpuDirectRDMACapable", ctypes.c_ubyte),
+                ("usage", ctypes.c_ushort)]
+
+
+class Prop(ctypes.Structure):       # hipMemAllocationProp (hip_runtime_api.h:1748)
+    _fields_ = [("type", ctypes.c_int), ("requestedHandleType", ctypes.c_int), ("location", Loc),
+                ("win32HandleMetaData", ctypes.c_void_p), ("allocFlags", AllocFlags)]
+
+
+class AccessDesc(ctypes.Structure):  # hipMemAccessDesc (hip_runtime_api.h:1201)
+    _fields_ = [("location", Loc), ("flags", ctypes.c_int)]
+
+
+@pytest.fixture(scope="module")
+def hip(cuda):
+    h = ctypes.CDLL("libamdhip64.so")
+    cuda.cuda.set_device(0)
+    cuda.zeros(1, device="cuda")        # the runtime up on device 0
+    return h
+
+
+def _ok(rc, what):
+    assert rc == 0, f"{what}: hip error {rc}"
+
+
+class Kinds:
+    """Allocations of each kind, freed at the end."""
+
+    def __init__(self, hip):
+        self.hip = hip
+        self.frees = []
+        self.keep = []
+
+    def device(self):
+        p = ctypes.c_void_p()
+        _ok(self.hip.hipMalloc(ctypes.byref(p), ctypes.c_size_t(NB)), "hipMalloc")
+        self.frees.append(("hipFree", p.value))
+        return p.value
+
+    def pool(self):
+        p = ctypes.c_void_p()
+        _ok(self.hip.hipMallocAsync(ctypes.byref(p), ctypes.c_size_t(NB), None), "hipMallocAsync")
+        _ok(self.hip.hipStreamSynchronize(None), "sync")
+        self.frees.append(("pool", p.value))
+        return p.value
+
+    def vmm(self):
+        prop = Prop()
+        prop.type = 1                   # hipMemAllocationTypePinned
+        prop.location = Loc(1, 0)       # hipMemLocationTypeDevice, device 0
+        gran = ctypes.c_size_t()
+        _ok(self.hip.hipMemGetAllocationGranularity(ctypes.byref(gran), ctypes.byref(prop), 0), "granularity")
+        size = (NB + gran.value - 1) // gran.value * gran.value
+        h = ctypes.c_void_p()
+        _ok(self.hip.hipMemCreate(ctypes.byref(h), ctypes.c_size_t(size), ctypes.byref(prop), ctypes.c_ulonglong(0)),
+            "hipMemCreate")
+        p = ctypes.c_void_p()
+        _ok(self.hip.hipMemAddressReserve(ctypes.byref(p), ctypes.c_size_t(size), ctypes.c_size_t(0), None,
+                                          ctypes.c_ulonglong(0)), "hipMemAddressReserve")
+        _ok(self.hip.hipMemMap(p, ctypes.c_size_t(size), ctypes.c_size_t(0), h, ctypes.c_ulonglong(0)), "hipMemMap")
+        acc = AccessDesc(Loc(1, 0), 3)  # hipMemAccessFlagsProtReadWrite
+        _ok(self.hip.hipMemSetAccess(p, ctypes.c_size_t(size), ctypes.byref(acc), ctypes.c_size_t(1)),
+            "hipMemSetAccess")
+        self.frees.append(("vmm", (p.value, size, h.value)))
+        return p.value
+
+    def managed(self):
+        p = ctypes.c_void_p()
+        _ok(self.hip.hipMallocManaged(ctypes.byref(p), ctypes.c_size_t(NB), 1), "hipMallocManaged")
+        self.frees.append(("hipFree", p.value))
+        return p.value
+
+    def pinned(self):
+        p = ctypes.c_void_p()
+        _ok(self.hip.hipHostMalloc(ctypes.byref(p), ctypes.c_size_t(NB), 0), "hipHostMalloc")
+        self.frees.append(("hipHostFree", p.value))
+        return p.value
+
+    def registered(self):
+        buf = np.zeros(NB + 8192, np.uint8)
+        addr = (buf.ctypes.data + 4095) & ~4095
+        _ok(self.hip.hipHostRegister(ctypes.c_void_p(addr), ctypes.c_size_t(NB), 0), "hipHostRegister")
+        self.keep.append(buf)
+        self.frees.append(("hipHostUnregister", addr))
+        return addr
+
+    def pageable(self):
+        buf = np.zeros(NB + 64, np.uint8)
+        self.keep.append(buf)
+        return buf.ctypes.data
+
+    def close(self):
+        self.hip.hipDeviceSynchronize()
+        for kind, v in reversed(self.frees):
+            if kind == "pool":
+                self.hip.hipFreeAsync(ctypes.c_void_p(v), None)
+                self.hip.hipStreamSynchronize(None)
+            elif kind == "vmm":
+                p, size, h = v
+                self.hip.hipMemUnmap(ctypes.c_void_p(p), ctypes.c_size_t(size))
+                self.hip.hipMemRelease(ctypes.c_void_p(h))
+                self.hip.hipMemAddressFree(ctypes.c_void_p(p), ctypes.c_size_t(size))
+            else:
+                getattr(self.hip, kind)(ctypes.c_void_p(v))
+
+
+KINDS = [("hipMalloc", "device", 1), ("hipMallocAsync", "pool", 1), ("VMM", "vmm", 1),
+         ("hipMallocManaged", "managed", 1), ("hipHostMalloc", "pinned", 0),
+         ("hipHostRegister", "registered", 0), ("pageable", "pageable", 0)]
+
+
+def _put(hip, dst, arr):
+    _ok(hip.hipMemcpy(ctypes.c_void_p(dst), ctypes.c_void_p(arr.ctypes.data), ctypes.c_size_t(NB), 4), "H2X")
+
+
+def _get(hip, src):
+    out = np.empty(N, np.float32)
+    _ok(hip.hipMemcpy(ctypes.c_void_p(out.ctypes.data), ctypes.c_void_p(src), ctypes.c_size_t(NB), 4), "X2H")
+    return out
+
+
+@pytest.mark.parametrize("name,maker,is_dev", KINDS, ids=[k[0] for k in KINDS])
+def test_kind_classified_and_reduced(mpi, orc, hip, name, maker, is_dev):
+    lib = mpi.load()
+    ks = Kinds(hip)
+    try:
+        x = getattr(ks, maker)()
+        y = getattr(ks, maker)()
+        d = ks.device()
+        assert lib.MPIR_Hip_is_device_ptr(ctypes.c_void_p(x)) == is_dev, name
+        rng = np.random.default_rng(sum(map(ord, name)))
+        a = rng.uniform(-1, 1, N).astype(np.float32)
+        b = rng.uniform(-1, 1, N).astype(np.float32)
+        want = a.copy()
+        assert orc.reduce_local(b.copy(), want, N, mpi.MPI_FLOAT, mpi.MPI_SUM) == 0
+        # (inbuf, inoutbuf): kind into device, device into kind, kind into kind
+        for pin, pio in ((x, d), (d, x), (y, x)):
+            _put(hip, pin, b)
+            _put(hip, pio, a)
+            rc = lib.MPI_Reduce_local(ctypes.c_void_p(pin), ctypes.c_void_p(pio), N, mpi.MPI_FLOAT, mpi.MPI_SUM)
+            assert rc == 0, mpi.error_string(rc)
+            got = _get(hip, pio)
+            assert np.array_equal(got.view(np.uint32), want.view(np.uint32)), (name, pin == x, pio == x)
+    finally:
+        ks.close()

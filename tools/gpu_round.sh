@@ -1,0 +1,48 @@
+#!/bin/bash
+# One GPU-box call of round 5's measurements: the steps named on the command
+# line, in order, each under its own time limit, stopping at the first failure.
+#   bash tools/gpu_round.sh TAG step...
+# steps:
+#   pytest     the whole -m gpu suite
+#   fused      the fused-combine / config-size GPU tests only
+#   classify   tools/classify_cost (pointer kinds: HSA vs HIP query)
+#   fold       tools/fold_trace (fused fold workgroup trace + candidate shapes)
+#   local      tools/local_ranks_ab.py (8 concurrent host-combine ranks)
+#   smoke      __graft_entry__.smoke()
+#   bench      python bench.py (defaults)
+#   prof       rocprofv3 --kernel-trace --stats of bench.py --steps 20
+#   lds        tools/lds_cap_cost (a fused fold beside a streaming kernel)
+#   hostlat    tools/host_small_latency gpu
+# Build every binary on the CPU side first (make -C mpich-pip_amd; hipcc lines
+# in each tool's header).
+set -o pipefail
+cd ${GRAFT_REPO_ROOT:-$PWD}
+TAG=${1:?tag}
+shift
+OUT=gpurun_out/$TAG
+mkdir -p $OUT
+export TMPDIR=/tmp
+for step in "$@"; do
+    echo "== $step $(date +%T)"
+    case $step in
+    pytest) timeout -k 10 420 python -u -m pytest -x -q -m gpu --timeout 120 --timeout-method thread tests/ \
+                > $OUT/pytest_gpu.log 2>&1; rc=$?; tail -2 $OUT/pytest_gpu.log ;;
+    fused) timeout -k 10 300 python -u -m pytest -x -q --timeout 200 --timeout-method thread \
+                tests/test_schedule_fused_gpu.py tests/test_coll_loopback_gpu.py tests/test_config_size_gpu.py \
+                > $OUT/pytest_fused.log 2>&1; rc=$?; tail -2 $OUT/pytest_fused.log ;;
+    classify) timeout -k 10 120 tools/classify_cost > $OUT/classify_cost.log 2>&1; rc=$?; cat $OUT/classify_cost.log ;;
+    fold) timeout -k 10 400 tools/fold_trace > $OUT/fold_trace.log 2>&1; rc=$?; cat $OUT/fold_trace.log ;;
+    local) timeout -k 10 400 python -u tools/local_ranks_ab.py 5 > $OUT/local_ranks_ab.log 2>&1; rc=$?
+           cat $OUT/local_ranks_ab.log ;;
+    smoke) timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1; rc=$?
+           tail -5 $OUT/smoke.log ;;
+    bench) timeout -k 10 400 python -u bench.py > $OUT/bench.log 2>&1; rc=$?; tail -c 3000 $OUT/bench.log ;;
+    prof) timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run -- python3 bench.py --steps 20 \
+                > $OUT/prof.log 2>&1; rc=$?; tail -3 $OUT/prof.log ;;
+    lds) timeout -k 10 300 tools/lds_cap_cost > $OUT/lds_cap_cost.log 2>&1; rc=$?; cat $OUT/lds_cap_cost.log ;;
+    hostlat) timeout -k 10 200 tools/host_small_latency gpu > $OUT/host_small_latency.log 2>&1; rc=$?
+             cat $OUT/host_small_latency.log ;;
+    *) echo "unknown step $step"; rc=2 ;;
+    esac
+    if [ $rc -ne 0 ]; then echo "step $step failed: $rc"; exit $rc; fi
+done
