@@ -120,9 +120,18 @@ struct DevCtx {
     size_t zc_bytes = 0;
 };
 
+// HIP's verdict on host pages the HSA query does not know (classify below)
+struct HostVerdict {
+    uintptr_t page = ~(uintptr_t)0;
+    int loc = 0;
+    int dev = 0;
+};
+constexpr int kVerdicts = 16;
+
 struct ThreadCtx {
     DevCtx dev[kMaxDev];
     char err[256] = {0};
+    HostVerdict verdict[kVerdicts];
     ThreadCtx *next = nullptr;
 };
 
@@ -147,6 +156,7 @@ struct CtxHolder {
                 g_pool = c->next;
                 c->next = nullptr;
                 c->err[0] = 0;
+                for (HostVerdict &v : c->verdict) v = HostVerdict();    // a new thread's own verdicts
             } else {
                 c = new ThreadCtx();
                 ++g_ctx_created;
@@ -661,6 +671,8 @@ struct AgentMap {
     int n = 0;
     uint64_t handle[kMaxDev];
     int dev[kMaxDev];
+    int ncpu = 0;
+    uint64_t cpu[kMaxDev];      // CPU agents (owners of host pools)
 };
 const AgentMap &agent_map() {
     static const AgentMap m = [] {
@@ -669,8 +681,13 @@ const AgentMap &agent_map() {
         std::vector<Gpu> gpus;
         (void)hsa_iterate_agents([](hsa_agent_t a, void *v) {
             hsa_device_type_t t;
-            if (hsa_agent_get_info(a, HSA_AGENT_INFO_DEVICE, &t) != HSA_STATUS_SUCCESS || t != HSA_DEVICE_TYPE_GPU)
+            if (hsa_agent_get_info(a, HSA_AGENT_INFO_DEVICE, &t) != HSA_STATUS_SUCCESS) return HSA_STATUS_SUCCESS;
+            if (t == HSA_DEVICE_TYPE_CPU) {
+                // a CPU agent: bdf 0xffffffff marks it (domain unused)
+                static_cast<std::vector<Gpu> *>(v)->push_back(Gpu{a.handle, ~0u, ~0u});
                 return HSA_STATUS_SUCCESS;
+            }
+            if (t != HSA_DEVICE_TYPE_GPU) return HSA_STATUS_SUCCESS;
             Gpu g{a.handle, 0, 0};
             if (hsa_agent_get_info(a, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_BDFID, &g.bdf) != HSA_STATUS_SUCCESS ||
                 hsa_agent_get_info(a, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_DOMAIN, &g.domain) != HSA_STATUS_SUCCESS)
@@ -678,9 +695,12 @@ const AgentMap &agent_map() {
             static_cast<std::vector<Gpu> *>(v)->push_back(g);
             return HSA_STATUS_SUCCESS;
         }, &gpus);
+        for (const Gpu &g : gpus)
+            if (g.bdf == ~0u && g.domain == ~0u && am.ncpu < kMaxDev) am.cpu[am.ncpu++] = g.handle;
         int ndev = 0;
         if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0 || ndev > kMaxDev) {
             (void)hipGetLastError();
+            am.n = 0;
             return am;
         }
         for (int d = 0; d < ndev; ++d) {
@@ -689,17 +709,21 @@ const AgentMap &agent_map() {
                 hipDeviceGetAttribute(&bus, hipDeviceAttributePciBusId, d) != hipSuccess ||
                 hipDeviceGetAttribute(&slot, hipDeviceAttributePciDeviceId, d) != hipSuccess) {
                 (void)hipGetLastError();
-                return AgentMap();
+                am.n = 0;
+                return am;
             }
             int hits = 0;
             for (const Gpu &g : gpus)
-                if (g.domain == (uint32_t)dom && ((g.bdf >> 8) & 0xff) == (uint32_t)bus &&
+                if (g.bdf != ~0u && g.domain == (uint32_t)dom && ((g.bdf >> 8) & 0xff) == (uint32_t)bus &&
                     ((g.bdf >> 3) & 0x1f) == (uint32_t)slot) {
                     am.handle[am.n] = g.handle;
                     am.dev[am.n] = d;
                     ++hits;
                 }
-            if (hits != 1) return AgentMap();
+            if (hits != 1) {
+                am.n = 0;
+                return am;
+            }
             ++am.n;
         }
         return am;
@@ -714,35 +738,62 @@ int agent_device(hsa_agent_t a) {
     return -1;
 }
 
+bool cpu_agent(hsa_agent_t a) {
+    const AgentMap &m = agent_map();
+    for (int i = 0; i < m.ncpu; ++i)
+        if (m.cpu[i] == a.handle) return true;
+    return false;
+}
+
 // Device memory (hipMalloc, stream-ordered pools, VMM mappings, IPC imports,
 // managed) is combined in place; host memory (pageable or pinned) takes the
 // host combine, the pinned slot or staging.  One HSA pointer query (24-66 ns
 // against HIP's 100-165, profiles/r05/classify_cost.log) answers for memory HSA
-// knows as a GPU's -- allocations of its pools (HSA), its virtual-memory
-// mappings (HSA_VMEM: stream-ordered pools, hipMemCreate + hipMemMap) and IPC imports
-// (hsa_ext_amd.h:2344-2372) -- and for memory it does not know at all (UNKNOWN),
-// which is host memory: pageable, or registered with hipHostRegister (HIP
-// registers without HSA's lock, so HSA reports it UNKNOWN; it is combined as
-// pageable memory, as MPICH itself treats a registered host buffer -- read in
-// place, no stream ordering).  Every other answer -- host pools (hipHostMalloc:
-// pinned, whose owning device orders the caller's null-stream work before the
-// read), managed memory (RESERVED_ADDR, no owner), graphics interop -- asks HIP.
+// knows as a GPU's: allocations of its pools (HSA), its virtual-memory mappings
+// (HSA_VMEM: stream-ordered pools, hipMemCreate + hipMemMap) and IPC imports
+// (hsa_ext_amd.h:2344-2372).  Every other answer asks HIP: host pools
+// (hipHostMalloc: pinned, whose owning device orders the caller's null-stream
+// work before the read), RESERVED_ADDR, graphics interop -- and UNKNOWN, which
+// is pageable memory, memory registered with hipHostRegister (HIP registers it
+// without HSA's lock), but also managed memory (hipMallocManaged answered
+// RESERVED_ADDR on one box and UNKNOWN on the next: profiles/r05/).  For host
+// pages -- UNKNOWN, LOCKED, or an allocation owned by a CPU agent -- HIP's host
+// verdicts (pageable, pinned) are kept per thread, keyed by the 4 KiB page: the
+// next call on the same host buffers costs the HSA query and a lookup.  Only
+// host verdicts are kept, and only looked up behind one of those answers, so a
+// stale one is harmless: a page that later becomes a GPU allocation answers HSA
+// as the GPU's, and one that becomes managed memory is host-accessible (the
+// host path reads it correctly); a device verdict is never reused.
 Loc classify(const void *p, int *dev) {
     if (!gpu_runtime_started()) return LOC_HOST;
     hsa_amd_pointer_info_t info;
     info.size = sizeof info;
-    if (hsa_amd_pointer_info(p, &info, nullptr, nullptr, nullptr) == HSA_STATUS_SUCCESS) {
-        if (info.type == HSA_EXT_POINTER_TYPE_UNKNOWN) return LOC_HOST;
-        if (info.type == HSA_EXT_POINTER_TYPE_HSA || info.type == HSA_EXT_POINTER_TYPE_HSA_VMEM ||
-            info.type == HSA_EXT_POINTER_TYPE_IPC) {
-            const int d = agent_device(info.agentOwner);
-            if (d >= 0) {
-                *dev = d;
-                return LOC_DEVICE;
-            }
+    const bool known = hsa_amd_pointer_info(p, &info, nullptr, nullptr, nullptr) == HSA_STATUS_SUCCESS;
+    if (known && (info.type == HSA_EXT_POINTER_TYPE_HSA || info.type == HSA_EXT_POINTER_TYPE_HSA_VMEM ||
+                  info.type == HSA_EXT_POINTER_TYPE_IPC)) {
+        const int d = agent_device(info.agentOwner);
+        if (d >= 0) {
+            *dev = d;
+            return LOC_DEVICE;
         }
     }
-    return classify_hip(p, dev);
+    const bool host_page = known && (info.type == HSA_EXT_POINTER_TYPE_UNKNOWN ||
+                                     info.type == HSA_EXT_POINTER_TYPE_LOCKED ||
+                                     (info.type == HSA_EXT_POINTER_TYPE_HSA && cpu_agent(info.agentOwner)));
+    if (!host_page) return classify_hip(p, dev);
+    const uintptr_t page = reinterpret_cast<uintptr_t>(p) >> 12;
+    HostVerdict &v = ctx().verdict[(page ^ (page >> 7)) & (kVerdicts - 1)];
+    if (v.page == page) {
+        *dev = v.dev;
+        return (Loc)v.loc;
+    }
+    const Loc l = classify_hip(p, dev);
+    if (l != LOC_DEVICE) {
+        v.page = page;
+        v.loc = l;
+        v.dev = l == LOC_PINNED ? *dev : 0;
+    }
+    return l;
 }
 
 // devices visible to this process (0 on a CPU-only rank: host operands are

@@ -9,9 +9,11 @@ Kinds: hipMalloc, hipMallocAsync (stream-ordered pool: HSA_VMEM), VMM
 hipHostRegister'ed malloc memory (UNKNOWN to HSA: pageable path) and plain
 pageable memory.  Each kind is paired with a hipMalloc buffer in both roles
 (inbuf and inoutbuf) and with a buffer of its own kind; MPIR_Hip_is_device_ptr
-reports the class.
+reports the class.  Each case runs on a thread of its own: the library keeps
+HIP's host verdicts per thread by page, and a fresh thread starts with none.
 """
 import ctypes
+import threading
 
 import numpy as np
 import pytest
@@ -150,6 +152,22 @@ def _get(hip, src):
 
 @pytest.mark.parametrize("name,maker,is_dev", KINDS, ids=[k[0] for k in KINDS])
 def test_kind_classified_and_reduced(mpi, orc, hip, name, maker, is_dev):
+    err = []
+
+    def body():
+        try:
+            _case(mpi, orc, hip, name, maker, is_dev)
+        except BaseException as e:      # noqa: BLE001
+            err.append(e)
+    t = threading.Thread(target=body)
+    t.start()
+    t.join(120)
+    assert not t.is_alive(), "case hung"
+    if err:
+        raise err[0]
+
+
+def _case(mpi, orc, hip, name, maker, is_dev):
     lib = mpi.load()
     ks = Kinds(hip)
     try:

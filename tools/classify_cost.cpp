@@ -105,5 +105,24 @@ int main() {
                (char *)info.agentBaseAddress <= (char *)k.p && (char *)k.p < (char *)info.agentBaseAddress + info.sizeInBytes,
                (t1 - t0) / N, (t2 - t1) / N);
     }
+    // hipMallocManaged at several sizes: HSA's answer at the base and inside
+    const size_t msz[4] = {MB, MB + 12, 64 * MB, 4096};
+    for (size_t sz : msz) {
+        void *m = nullptr;
+        if (hipMallocManaged(&m, sz) != hipSuccess) {
+            (void)hipGetLastError();
+            continue;
+        }
+        int types[2];
+        for (int i = 0; i < 2; ++i) {
+            hsa_amd_pointer_info_t info;
+            memset(&info, 0, sizeof info);
+            info.size = sizeof info;
+            (void)hsa_amd_pointer_info((char *)m + (i ? sz / 2 : 0), &info, nullptr, nullptr, nullptr);
+            types[i] = (int)info.type;
+        }
+        printf("hipMallocManaged %9zu B: hsa type at base %d, mid %d\n", sz, types[0], types[1]);
+        (void)hipFree(m);
+    }
     return 0;
 }
