@@ -10,7 +10,7 @@
 #   local      tools/local_ranks_ab.py (8 concurrent host-combine ranks)
 #   smoke      __graft_entry__.smoke()
 #   bench      python bench.py (defaults)
-#   prof       rocprofv3 --kernel-trace --stats of bench.py --steps 20
+#   prof       tools/profile_r03.sh: kernel trace + stats at 256 / 64 MiB, FETCH_SIZE and WRITE_SIZE passes
 #   lds        tools/lds_cap_cost (a fused fold beside a streaming kernel)
 #   hostlat    tools/host_small_latency gpu
 # Build every binary on the CPU side first (make -C mpich-pip_amd; hipcc lines
@@ -37,8 +37,7 @@ for step in "$@"; do
     smoke) timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1; rc=$?
            tail -5 $OUT/smoke.log ;;
     bench) timeout -k 10 400 python -u bench.py > $OUT/bench.log 2>&1; rc=$?; tail -c 3000 $OUT/bench.log ;;
-    prof) timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run -- python3 bench.py --steps 20 \
-                > $OUT/prof.log 2>&1; rc=$?; tail -3 $OUT/prof.log ;;
+    prof) timeout -k 10 1100 bash tools/profile_r03.sh $TAG > $OUT/prof.log 2>&1; rc=$?; tail -3 $OUT/prof.log ;;
     lds) timeout -k 10 300 tools/lds_cap_cost > $OUT/lds_cap_cost.log 2>&1; rc=$?; cat $OUT/lds_cap_cost.log ;;
     hostlat) timeout -k 10 200 tools/host_small_latency gpu > $OUT/host_small_latency.log 2>&1; rc=$?
              cat $OUT/host_small_latency.log ;;
