@@ -714,7 +714,11 @@ def cpu_baseline(args, count: int, alg_bytes: int) -> dict:
                 "per_socket": {str(k): round(bpt * len(v) / max(v) / GIB, 2) for k, v in sorted(sockets.items())},
                 "seconds": round(max(secs), 3)}
 
-    per = count - count % 64
+    # at most 16 GiB of operands over all threads (two per thread): a node whose
+    # quota grants many cores (an 8-GPU node) gets smaller per-thread operands,
+    # still far past every cache
+    per = min(count, (16 << 30) // (8 * len(cores)))
+    per -= per % 64
     g = run(cores, per, iters, "gcc")
     if g is None:
         return {"error": "cpu baseline thread failure"}

@@ -1,4 +1,4 @@
-"""The committed bench line (profiles/r04/bench_r04i.log, measured on MI355X) against
+"""The committed bench line (profiles/r05/bench_r05b.log, measured on MI355X) against
 the driver's contract and against itself: BASELINE.json's metric, the
 required keys, value = algorithmic bytes x N / time, roofline.frac =
 achieved / peak with achieved = 805,306,368 B / mean launch time, and the
@@ -10,7 +10,7 @@ import os
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LINE = os.path.join(ROOT, "profiles", "r04", "bench_r04i.log")
+LINE = os.path.join(ROOT, "profiles", "r05", "bench_r05b.log")
 GIB = float(1 << 30)
 
 
@@ -83,3 +83,21 @@ def test_per_rank_and_config5_blocks(line):
         b = c5[key]
         assert b["frac"] == pytest.approx(alg / (b["kernel_us"] * 1e-6) / 8.0e12, rel=2e-3)
         assert 1.0 <= b["traffic_over_algorithmic"] < 1.01
+
+
+def test_call_distribution(line):
+    """Round 5 (VERDICT r4 #3c): the K timed calls one by one, and the mean call
+    split into the kernel's CP-timestamped mean + a fixed remainder."""
+    cd = line["call_distribution"]
+    assert cd["calls"] == line["steps"]
+    assert cd["min_us"] <= cd["p10_us"] <= cd["median_us"] <= cd["p90_us"] <= cd["max_us"]
+    # the stamps' mean is the loop's own mean (one clock read per call inside it)
+    assert cd["mean_us"] == pytest.approx(line["ms_per_step"] * 1e3, rel=5e-3)
+    alg = line["config"]["algorithmic_bytes_per_call"]
+    assert cd["frac_of_hbm_peak_at_median"] == pytest.approx(alg / (cd["median_us"] * 1e-6) / 8.0e12, rel=2e-3)
+    d = cd["decomposition"]
+    assert d["kernel_mean_us"] == pytest.approx(line["roofline"]["mean_launch_us"], abs=0.01)
+    assert d["call_mean_us"] == pytest.approx(d["kernel_mean_us"] + d["fixed_us"], abs=0.02)
+    assert d["kernel_us_for_call_at_0.80"] == pytest.approx(alg / (0.8 * 8.0e12) * 1e6 - d["fixed_us"], abs=0.02)
+    pr = line["per_rank"][0]
+    assert pr["call_median_us"] == cd["median_us"] and pr["call_p10_p90_us"] == [cd["p10_us"], cd["p90_us"]]

@@ -29,6 +29,8 @@
 //                 the current tile's fold and store (software pipeline), tiles
 //                 interleaved over the grid
 // for CHAIN8 fp16 8 x 128 MiB (config 5) and TREE8 fp32 8 x 32 MiB (config 4).
+//
+// Part 3, write volume: the fold's eight reads with 0, 1 and 2 output streams.
 #include <hip/hip_runtime.h>
 #include <algorithm>
 #include <cstdio>
@@ -133,6 +135,49 @@ __global__ __launch_bounds__(kThreads) void k_fold_persist(MultiArgs a, uint64_t
         if (blk + g < ntiles) fold_load<T, 8, U>(x, a, blk + g);
         fold_store<T, 8, TREE, U>(y, a, blk);
         blk += g;
+    }
+}
+
+// ---- write-volume probe: the product fold (1024 threads, U = 1) with NW output
+// streams: 0 (the eight reads alone; a store only for an impossible result, so
+// the loads stay live), 1 (the product), 2 (the result to out and to out2)
+template <int NW>
+__global__ __launch_bounds__(1024) void k_fold_nw(MultiArgs a, char *out2) {
+    constexpr uint32_t tile = 1024 * 16;
+    const uint64_t base = (uint64_t)blockIdx.x * tile;
+    if (base >= a.vbytes) return;
+    const uint64_t left = a.vbytes - base;
+    const int nrec = (int)(left < tile ? left : tile);
+    const int t = (int)threadIdx.x;
+    const int wb = (t >> 6) * 1024 + (t & 63) * 16;
+    u32x4 x[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void *)(a.in[j] + base), 0, nrec, 0x00020000);
+        x[j] = __builtin_amdgcn_raw_buffer_load_b128(r, wb, 0, kCachePolicyNT);
+        if ((j + 1) % 4 == 0 && j + 1 < 8) issue_gap();
+    }
+    Pack16<f16> pk[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) pk[j] = __builtin_bit_cast(Pack16<f16>, x[j]);
+    Pack16<f16> res;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        f16 e[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) e[j] = pk[j].e[k];
+        res.e[k] = fold_fast<OpSum, f16, 8, false>(e);
+    }
+    const u32x4 v = __builtin_bit_cast(u32x4, res);
+    __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc((void *)(a.out + base), 0, nrec, 0x00020000);
+    if (NW == 0) {
+        if (__builtin_expect(v.x == 0xFFFFFFFFu && v.y == 0x01234567u, 0)) store16(v, ro, wb, false);
+    } else {
+        store16(v, ro, wb, false);
+        if (NW == 2) {
+            __amdgpu_buffer_rsrc_t r2 = __builtin_amdgcn_make_buffer_rsrc((void *)(out2 + base), 0, nrec, 0x00020000);
+            store16(v, r2, wb, false);
+        }
     }
 }
 
@@ -423,6 +468,66 @@ int main(int argc, char **argv) {
             printf("  %-28s median %8.2f us  min %8.2f  frac of 8 TB/s %.4f\n", kVarNames[v], med, us[v][0],
                    bytes / (med * 1e-6) / 8e12);
         }
+        for (auto p : sets) CK(hipFree(p));
+    }
+
+    // ---------------- part 3: write volume ------------------------------------
+    // the fold's eight reads with 0 / 1 / 2 output streams (nt stores), CHAIN8
+    // fp16 over 8 x 128 MiB: if the mix, not the bytes, sets the rate, a second
+    // write stream costs less than its bytes at the fold's rate
+    {
+        CK(hipFuncSetAttribute((const void *)k_fold_nw<0>, hipFuncAttributeMaxDynamicSharedMemorySize, 96 << 10));
+        CK(hipFuncSetAttribute((const void *)k_fold_nw<1>, hipFuncAttributeMaxDynamicSharedMemorySize, 96 << 10));
+        CK(hipFuncSetAttribute((const void *)k_fold_nw<2>, hipFuncAttributeMaxDynamicSharedMemorySize, 96 << 10));
+        const uint64_t block = 128ull << 20, stride = block + 4352, setbytes = 8 * stride + 2 * block + 4352;
+        const int nsets = 3;
+        std::vector<char *> sets(nsets);
+        for (auto &p : sets) {
+            CK(hipMalloc(&p, setbytes));
+            k_fill<<<4096, 256>>>((uint16_t *)p, setbytes / 2, (uint32_t)(uintptr_t)p, 1);
+        }
+        CK(hipDeviceSynchronize());
+        const unsigned groups = (unsigned)(block / 16384);
+        auto run = [&](int k, int nw) {
+            MultiArgs a{};
+            char *b = sets[k % nsets];
+            for (int j = 0; j < 8; ++j) a.in[j] = b + j * stride;
+            a.out = b + 8 * stride;
+            a.vbytes = block;
+            char *o2 = b + 8 * stride + block + 4352;
+            if (nw == 0) hipLaunchKernelGGL(k_fold_nw<0>, dim3(groups), dim3(1024), 96 << 10, s, a, o2);
+            else if (nw == 1) hipLaunchKernelGGL(k_fold_nw<1>, dim3(groups), dim3(1024), 96 << 10, s, a, o2);
+            else hipLaunchKernelGGL(k_fold_nw<2>, dim3(groups), dim3(1024), 96 << 10, s, a, o2);
+        };
+        std::vector<double> us[3];
+        std::mt19937 rng(5);
+        int k = 0;
+        const int batch = 20;
+        for (int r = 0; r < 11; ++r) {
+            int order[3] = {0, 1, 2};
+            std::shuffle(order, order + 3, rng);
+            for (int nw : order) {
+                run(k++, nw);
+                CK(hipEventRecord(e0, s));
+                for (int b = 0; b < batch; ++b) run(k++, nw);
+                CK(hipEventRecord(e1, s));
+                CK(hipEventSynchronize(e1));
+                float ms = 0;
+                CK(hipEventElapsedTime(&ms, e0, e1));
+                if (r) us[nw].push_back(ms * 1e3 / batch);
+            }
+        }
+        printf("write volume: CHAIN8 fp16 8 x 128 MiB reads + 0 / 1 / 2 nt output streams (1 workgroup / CU), "
+               "10 rounds x %d launches\n", batch);
+        double med[3];
+        for (int nw = 0; nw < 3; ++nw) {
+            std::sort(us[nw].begin(), us[nw].end());
+            med[nw] = us[nw][us[nw].size() / 2];
+            const double bytes = (8.0 + nw) * block;
+            printf("  8R + %dW  median %8.2f us  frac of 8 TB/s %.4f\n", nw, med[nw], bytes / (med[nw] * 1e-6) / 8e12);
+        }
+        printf("  the first write stream costs %.2f us (%.2f us at the reads' rate), the second %.2f us\n",
+               med[1] - med[0], med[0] / 8.0, med[2] - med[1]);
         for (auto p : sets) CK(hipFree(p));
     }
     return 0;
