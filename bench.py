@@ -41,7 +41,7 @@ Extra fields (rank 0):
                 bytes from the committed rocprofv3 PMC summary (profiles/).
   stream_api    the same combine enqueued back-to-back with MPIX_Reduce_local_stream
                 (the async variant the library's own schedules use).
-  pcie_inclusive  pinned / pageable host buffers -> MPI_Reduce_local forced onto the
+  pcie_inclusive  pinned / pageable / registered host buffers -> MPI_Reduce_local forced onto the
                 GPU (host limit 0: H2D + kernel + D2H), the rate when rank buffers
                 arrive in host memory over PiP shm.  Reported for DESIGN.md; never
                 `value`.
@@ -1040,14 +1040,29 @@ def main():
         try:
             dth = time_steps(hstep, hk, 1, sync, barrier, max_over_ranks)
             dtp = time_steps(pstep, hk, 1, sync, barrier, max_over_ranks)
+            # the same pageable pages registered with hipHostRegister: how a PiP /
+            # shm segment is pinned in place (SURVEY.md §8d host-inclusive rate)
+            hip = ctypes.CDLL("libamdhip64.so")
+            regd = []
+            for arr in (pa, pb):
+                if hip.hipHostRegister(ctypes.c_void_p(arr.ctypes.data), ctypes.c_size_t(arr.nbytes), 0) == 0:
+                    regd.append(arr)
+            try:
+                dtr = time_steps(pstep, hk, 1, sync, barrier, max_over_ranks) if len(regd) == 2 else None
+            finally:
+                for arr in regd:
+                    hip.hipHostUnregister(ctypes.c_void_p(arr.ctypes.data))
         finally:
             lib.MPIR_Hip_set_host_max_bytes(prev)
         out["pcie_inclusive"] = {"value": round(alg_bytes * hk * world / dth / GIB, 2), "unit": "GiB/s",
                                  "ms_per_step": round(dth / hk * 1e3, 3),
                                  "pageable_value": round(alg_bytes * hk * world / dtp / GIB, 2),
                                  "pageable_ms_per_step": round(dtp / hk * 1e3, 3),
+                                 "registered_value": round(alg_bytes * hk * world / dtr / GIB, 2) if dtr else None,
+                                 "registered_ms_per_step": round(dtr / hk * 1e3, 3) if dtr else None,
                                  "note": "host in/inout forced onto the GPU (host limit 0): 16 MiB chunks through "
-                                         "the up (H2D x2) / comp / down (D2H) stream pipeline; pinned DMA'd directly, "
+                                         "the up (H2D x2) / comp / down (D2H) stream pipeline; pinned (hipHostMalloc) "
+                                         "and registered (hipHostRegister'ed pageable pages) DMA'd directly, "
                                          "pageable via pinned bounce slots filled and drained by 4 copy threads"}
         # the default dispatch for the same host buffers: the host combine
         dhh = time_steps(hstep, hk, 1, sync, barrier, max_over_ranks)

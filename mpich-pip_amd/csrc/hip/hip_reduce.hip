@@ -364,10 +364,10 @@ int local_ranks() {
 // Host-combine threads for one rank, from the CPUs the node's L local ranks
 // share (the reference's combine is one thread per rank,
 // opsum.c:21-76):
-//   * affinity: a mask of m of the node's c online CPUs.  Ranks bound to
-//     disjoint sets (L * m <= c) each own their mask; unbound ranks (m = c)
-//     share it L ways; in between (e.g. --bind-to socket) ceil(L * m / c)
-//     ranks share each mask;
+//   * affinity: a mask of m of the c CPUs the job may use (the cgroup's cpuset,
+//     else the online CPUs).  Ranks bound to disjoint sets (L * m <= c) each
+//     own their mask; unbound ranks (m = c) share it L ways; in between (e.g.
+//     --bind-to socket) ceil(L * m / c) ranks share each mask;
 //   * cgroup quota q (cpu.max): the job's or container's, shared by all L.
 // The share is at most 16 (the host combine's measured scaling: 256 MiB fp32
 // SUM, 16-CPU quota, 131-136 GiB/s on 4 threads, 259-299 on 16;
@@ -382,22 +382,37 @@ int local_ranks() {
 // them, never beside a NUMA node's pool that does the work; the size is fixed
 // at the first call, so MPIR_Hip_set_local_ranks() acts before the first host
 // combine)
+int parse_cpulist(const char *path, std::vector<int> &out);
+// The CPUs the job's ranks can share: the cgroup's cpuset (a container pinned
+// to 16 of the host's 256 CPUs gives every unbound rank that same 16-CPU mask),
+// else the online CPUs
 int online_cpus() {
+    for (const char *path : {"/sys/fs/cgroup/cpuset.cpus.effective", "/sys/fs/cgroup/cpuset/cpuset.effective_cpus"}) {
+        std::vector<int> cpus;
+        if (parse_cpulist(path, cpus) == 0 && !cpus.empty()) return (int)cpus.size();
+    }
     const long n = sysconf(_SC_NPROCESSORS_ONLN);
     return n >= 1 ? (int)n : 1;
 }
+// the cgroup's CPU quota in CPUs (v2 cpu.max "quota period", v1 cfs_quota_us /
+// cfs_period_us), 0 if none
 int cgroup_quota_cpus() {
-    int q = 0;
+    long quota = -1, period = 0;
     if (FILE *f = fopen("/sys/fs/cgroup/cpu.max", "r")) {
-        char quota[32];
-        long period = 0;
-        if (fscanf(f, "%31s %ld", quota, &period) == 2 && strcmp(quota, "max") != 0 && period > 0) {
-            const long v = (atol(quota) + period - 1) / period;
-            if (v >= 1 && v < (1L << 20)) q = (int)v;
-        }
+        char q[32];
+        if (fscanf(f, "%31s %ld", q, &period) == 2 && strcmp(q, "max") != 0) quota = atol(q);
         fclose(f);
+    } else if (FILE *fq = fopen("/sys/fs/cgroup/cpu/cpu.cfs_quota_us", "r")) {
+        if (fscanf(fq, "%ld", &quota) != 1) quota = -1;
+        fclose(fq);
+        if (FILE *fp = fopen("/sys/fs/cgroup/cpu/cpu.cfs_period_us", "r")) {
+            if (fscanf(fp, "%ld", &period) != 1) period = 0;
+            fclose(fp);
+        }
     }
-    return q;
+    if (quota <= 0 || period <= 0) return 0;
+    const long v = (quota + period - 1) / period;
+    return v >= 1 && v < (1L << 20) ? (int)v : 0;
 }
 int share_threads(int mask, int online, int quota, int L) {
     if (L < 1) L = 1;

@@ -56,16 +56,47 @@ print(json.dumps({{"rank": rank, "workers": after - before, "pool": lib.MPIR_Hip
 """
 
 
+def _cpulist(path: str) -> int:
+    try:
+        txt = open(path).read().strip()
+    except OSError:
+        return 0
+    n = 0
+    for part in txt.split(","):
+        if not part:
+            continue
+        a, _, b = part.partition("-")
+        n += int(b or a) - int(a) + 1
+    return n
+
+
+def job_cpus() -> int:
+    """The CPUs the job's ranks share, as the library counts them
+    (hip_reduce.hip online_cpus): the cgroup's cpuset, else the online CPUs."""
+    for path in ("/sys/fs/cgroup/cpuset.cpus.effective", "/sys/fs/cgroup/cpuset/cpuset.effective_cpus"):
+        n = _cpulist(path)
+        if n:
+            return n
+    return os.cpu_count()
+
+
 def usable_cpus() -> int:
-    """This process's affinity mask, capped by a cgroup v2 quota."""
+    """This process's affinity mask, capped by a cgroup CPU quota (v2 or v1)."""
     n = len(os.sched_getaffinity(0))
+    quota = period = 0
     try:
         with open("/sys/fs/cgroup/cpu.max") as f:
-            quota, period = f.read().split()[:2]
-        if quota != "max":
-            n = min(n, -(-int(quota) // int(period)))
+            q, p = f.read().split()[:2]
+        if q != "max":
+            quota, period = int(q), int(p)
     except (OSError, ValueError):
-        pass
+        try:
+            quota = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+            period = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+        except (OSError, ValueError):
+            pass
+    if quota > 0 and period > 0:
+        n = min(n, -(-quota // period))
     return n
 
 

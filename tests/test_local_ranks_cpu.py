@@ -61,13 +61,13 @@ def _pool(cpus, env_extra):
 
 def _quota():
     q = _local_ranks.usable_cpus()
-    return q if q < os.cpu_count() else None
+    return q if q < len(os.sched_getaffinity(0)) else None
 
 
-@pytest.mark.skipif(len(os.sched_getaffinity(0)) < 8 or len(os.sched_getaffinity(0)) != os.cpu_count(),
+@pytest.mark.skipif(len(os.sched_getaffinity(0)) < 8 or len(os.sched_getaffinity(0)) != _local_ranks.job_cpus(),
                     reason="needs an unbound process on a node of >= 8 CPUs")
 def test_sizing_rule():
-    c = os.cpu_count()
+    c = _local_ranks.job_cpus()
     q = _quota()
     full = list(range(c))
 
