@@ -34,3 +34,15 @@ def test_every_variable_is_documented():
         if n not in doc and not (short and short in doc):
             missing.append(n)
     assert not missing, f"read by the library but not in INTEGRATION.md: {missing}"
+
+
+def test_local_rank_variables_documented():
+    """The launchers' node-local rank counts the host pool reads (round 5;
+    hip_reduce.hip local_ranks reads them in a loop the scan above cannot see)."""
+    with open(os.path.join(ROOT, "mpich-pip_amd", "csrc", "hip", "hip_reduce.hip"), encoding="utf-8") as fh:
+        src = fh.read()
+    with open(os.path.join(ROOT, "INTEGRATION.md"), encoding="utf-8") as fh:
+        doc = fh.read()
+    for name in ("MPI_LOCALNRANKS", "MPIR_PIP_SIZE", "LOCAL_WORLD_SIZE", "OMPI_COMM_WORLD_LOCAL_SIZE"):
+        assert f'"{name}"' in src, name
+        assert name in doc, name
