@@ -33,3 +33,7 @@ def test_bench_two_ranks_share_one_gpu():
     pr = out["per_rank"]
     assert [r["rank"] for r in pr] == [0, 1], pr
     assert all(r["seconds"] > 0 and r["direct_state"] in (1, 2) and r["direct_share"] == 1.0 for r in pr), pr
+    # round 5: each rank's call distribution, and the CPU baseline beside the parked rank
+    assert all(r["call_median_us"] > 0 and len(r["call_p10_p90_us"]) == 2 for r in pr), pr
+    assert out["call_distribution"]["calls"] == 4
+    assert out["cpu_baseline"]["ranks_parked"] == 1 and out["cpu_baseline"]["value"] > 0
