@@ -1042,7 +1042,7 @@ def main():
             dtp = time_steps(pstep, hk, 1, sync, barrier, max_over_ranks)
             # the same pageable pages registered with hipHostRegister: how a PiP /
             # shm segment is pinned in place (SURVEY.md §8d host-inclusive rate)
-            hip = ctypes.CDLL("libamdhip64.so")
+            hip = ctypes.CDLL("libamdhip64.so.7")   # the library's own HIP runtime, not torch's bundled copy
             regd = []
             for arr in (pa, pb):
                 if hip.hipHostRegister(ctypes.c_void_p(arr.ctypes.data), ctypes.c_size_t(arr.nbytes), 0) == 0:

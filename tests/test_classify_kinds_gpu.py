@@ -11,6 +11,14 @@ pageable memory.  Each kind is paired with a hipMalloc buffer in both roles
 (inbuf and inoutbuf) and with a buffer of its own kind; MPIR_Hip_is_device_ptr
 reports the class.  Each case runs on a thread of its own: the library keeps
 HIP's host verdicts per thread by page, and a fresh thread starts with none.
+
+The buffers come from the HIP runtime the library itself links
+(libamdhip64.so.7 from /opt/rocm), not from the copy torch bundles: a process
+that imports torch holds two HIP runtimes (and two HSA runtimes), and one does
+not know the other's managed or pinned allocations (it sees them through the
+kernel driver only: another runtime's hipHostMalloc memory reads as device
+memory, its managed memory as unregistered host memory -- both still combined
+correctly, on the GPU or the host).  An MPI program has one runtime.
 """
 import ctypes
 import threading
@@ -42,12 +50,48 @@ class AccessDesc(ctypes.Structure):  # hipMemAccessDesc (hip_runtime_api.h:1201)
     _fields_ = [("location", Loc), ("flags", ctypes.c_int)]
 
 
+def library_hip(mpi):
+    """The HIP runtime the product library links (already loaded by it)."""
+    mpi.load()
+    return ctypes.CDLL("libamdhip64.so.7")
+
+
 @pytest.fixture(scope="module")
-def hip(cuda):
-    h = ctypes.CDLL("libamdhip64.so")
-    cuda.cuda.set_device(0)
-    cuda.zeros(1, device="cuda")        # the runtime up on device 0
+def hip(mpi):
+    if mpi.load().MPIR_Hip_device_count() <= 0:
+        pytest.fail("gpu test requires a HIP device")
+    h = library_hip(mpi)
+    _ok(h.hipSetDevice(0), "hipSetDevice")
     return h
+
+
+class PtrAttr(ctypes.Structure):     # hipPointerAttribute_t (hip_runtime_api.h:280)
+    _fields_ = [("type", ctypes.c_int), ("device", ctypes.c_int), ("devicePointer", ctypes.c_void_p),
+                ("hostPointer", ctypes.c_void_p), ("isManaged", ctypes.c_int), ("allocationFlags", ctypes.c_uint)]
+
+
+class HsaInfo(ctypes.Structure):     # hsa_amd_pointer_info_t (hsa_ext_amd.h:2379)
+    _fields_ = [("size", ctypes.c_uint32), ("type", ctypes.c_int), ("agentBaseAddress", ctypes.c_void_p),
+                ("hostBaseAddress", ctypes.c_void_p), ("sizeInBytes", ctypes.c_size_t), ("userData", ctypes.c_void_p),
+                ("agentOwner", ctypes.c_uint64), ("global_flags", ctypes.c_uint32), ("registered", ctypes.c_bool)]
+
+
+def _diag(hip, p):
+    """HIP's and HSA's own answers for p (for the failure message)."""
+    at = PtrAttr()
+    rc = hip.hipPointerGetAttributes(ctypes.byref(at), ctypes.c_void_p(p))
+    hsa = ctypes.CDLL("libhsa-runtime64.so.1")     # the library's HSA runtime
+    info = HsaInfo()
+    info.size = ctypes.sizeof(info)
+    hrc = hsa.hsa_amd_pointer_info(ctypes.c_void_p(p), ctypes.byref(info), None, None, None)
+    class Agent(ctypes.Structure):
+        _fields_ = [("handle", ctypes.c_uint64)]
+    kind = ctypes.c_int(-1)
+    if info.agentOwner:
+        hsa.hsa_agent_get_info(Agent(info.agentOwner), 17, ctypes.byref(kind))     # HSA_AGENT_INFO_DEVICE
+    return (f"ptr {p:#x}: hip rc {rc} type {at.type} device {at.device} managed {at.isManaged}; "
+            f"hsa rc {hrc} type {info.type} owner {info.agentOwner:#x} ({ {0: 'cpu', 1: 'gpu'}.get(kind.value, '-') }) "
+            f"flags {info.global_flags:#x}")
 
 
 def _ok(rc, what):
@@ -174,7 +218,9 @@ def _case(mpi, orc, hip, name, maker, is_dev):
         x = getattr(ks, maker)()
         y = getattr(ks, maker)()
         d = ks.device()
-        assert lib.MPIR_Hip_is_device_ptr(ctypes.c_void_p(x)) == is_dev, name
+        pre = _diag(hip, x)
+        got = lib.MPIR_Hip_is_device_ptr(ctypes.c_void_p(x))
+        assert got == is_dev, (name, pre, _diag(hip, x), lib.MPIR_Hip_is_device_ptr(ctypes.c_void_p(x)))
         rng = np.random.default_rng(sum(map(ord, name)))
         a = rng.uniform(-1, 1, N).astype(np.float32)
         b = rng.uniform(-1, 1, N).astype(np.float32)
