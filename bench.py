@@ -169,7 +169,10 @@ def cpu_standin(args) -> None:
                               "rccl": bench_coll.coll_row(per, world, alg, "reduce_scatter")}}
     if rank == 0 and not args.no_cpu_baseline:
         # the real baseline routine on a small sample
-        out["cpu_baseline"] = cpu_baseline(args, 1 << 16, 3 * (1 << 18))
+        try:
+            out["cpu_baseline"] = cpu_baseline(args, 1 << 16, 3 * (1 << 18))
+        except Exception as exc:        # noqa: BLE001
+            out["cpu_baseline"] = {"error": repr(exc)}
         out["cpu_baseline"]["ranks_parked"] = world - 1
     if not args.no_cpu_baseline:
         park_until_rank0(world > 1, world, rank, dist, "bench_cpu_baseline_done")
@@ -294,7 +297,7 @@ def call_stats(calls: list, alg_bytes: int) -> dict:
             "frac_of_hbm_peak_at_median": round(alg_bytes / med / HBM_PEAK_BPS, 4)}
 
 
-def park_until_rank0(use_pg: bool, world: int, rank: int, dist, key: str, timeout_s: float = 900.0):
+def park_until_rank0(use_pg: bool, world: int, rank: int, dist, key: str, timeout_s: float = 600.0):
     """Ranks other than 0 wait for rank 0's `key` on the process group's store
     (a blocking socket read, no spin), so rank 0's CPU work runs beside idle
     ranks; rank 0 sets it.  Falls back to a barrier if the store is unavailable."""
@@ -1083,7 +1086,10 @@ def main():
     # the CPU baseline on rank 0 at every N, after the GPU work, the other
     # ranks parked on a blocking store read (no spinning core beside it)
     if rank == 0 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(args, count, alg_bytes)
+        try:
+            out["cpu_baseline"] = cpu_baseline(args, count, alg_bytes)
+        except Exception as exc:        # noqa: BLE001  (the parked ranks must still be released)
+            out["cpu_baseline"] = {"error": repr(exc)}
         if world > 1:
             out["cpu_baseline"]["ranks_parked"] = world - 1
     if not args.no_cpu_baseline:
