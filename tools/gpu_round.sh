@@ -13,6 +13,7 @@
 #   prof       tools/profile_r03.sh: kernel trace + stats at 256 / 64 MiB, FETCH_SIZE and WRITE_SIZE passes
 #   lds        tools/lds_cap_cost (a fused fold beside a streaming kernel)
 #   hostlat    tools/host_small_latency gpu
+#   driver6    python bench.py --steps 20 --warmup 5 (the driver's shape), six fresh processes
 # Build every binary on the CPU side first (make -C mpich-pip_amd; hipcc lines
 # in each tool's header).
 set -o pipefail
@@ -41,6 +42,17 @@ for step in "$@"; do
     lds) timeout -k 10 300 tools/lds_cap_cost > $OUT/lds_cap_cost.log 2>&1; rc=$?; cat $OUT/lds_cap_cost.log ;;
     hostlat) timeout -k 10 200 tools/host_small_latency gpu > $OUT/host_small_latency.log 2>&1; rc=$?
              cat $OUT/host_small_latency.log ;;
+    driver6) rc=0
+             for i in 1 2 3 4 5 6; do
+                 timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 > $OUT/bench_ds_$i.log 2>&1 || { rc=$?; break; }
+                 python - $OUT/bench_ds_$i.log <<'PY'
+import json, sys
+d = [json.loads(l) for l in open(sys.argv[1]) if l.startswith("{")][-1]
+c = d["call_distribution"]
+print(f"{sys.argv[1]}: value {d['value']} = {d['per_gpu']['frac_of_hbm_peak']}, kernel {d['roofline']['mean_launch_us']} us "
+      f"({d['roofline']['frac']}), call median {c['median_us']} p90 {c['p90_us']}, fixed {c['decomposition']['fixed_us']}")
+PY
+             done ;;
     *) echo "unknown step $step"; rc=2 ;;
     esac
     if [ $rc -ne 0 ]; then echo "step $step failed: $rc"; exit $rc; fi
