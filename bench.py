@@ -285,16 +285,27 @@ def time_loop(run, k: int, w: int, sync, barrier, max_over_ranks, own: list | No
     return max_over_ranks(t1 - t0)
 
 
-def call_stats(calls: list, alg_bytes: int) -> dict:
+def call_stats(calls: list, alg_bytes: int, pair_of: list | None = None) -> dict:
     """The timed calls' own distribution: median, p10 / p90,
-    mean, min / max in us, and the median call's fraction of the HBM peak."""
+    mean, min / max in us, the median call's fraction of the HBM peak, the share
+    of slow calls (> median + 4 us) and what they add to the mean call; with
+    `pair_of` (each call's operand pair), the median per pair."""
     v = sorted(calls)
     n = len(v)
     med = v[n // 2]
-    return {"calls": n, "median_us": round(med * 1e6, 2), "p10_us": round(v[n // 10] * 1e6, 2),
-            "p90_us": round(v[min(n - 1, (n * 9) // 10)] * 1e6, 2), "mean_us": round(sum(v) / n * 1e6, 2),
-            "min_us": round(v[0] * 1e6, 2), "max_us": round(v[-1] * 1e6, 2),
-            "frac_of_hbm_peak_at_median": round(alg_bytes / med / HBM_PEAK_BPS, 4)}
+    slow = [x for x in calls if x > med + 4e-6]
+    out = {"calls": n, "median_us": round(med * 1e6, 2), "p10_us": round(v[n // 10] * 1e6, 2),
+           "p90_us": round(v[min(n - 1, (n * 9) // 10)] * 1e6, 2), "mean_us": round(sum(v) / n * 1e6, 2),
+           "min_us": round(v[0] * 1e6, 2), "max_us": round(v[-1] * 1e6, 2),
+           "frac_of_hbm_peak_at_median": round(alg_bytes / med / HBM_PEAK_BPS, 4),
+           "slow_share": round(len(slow) / n, 4),
+           "slow_excess_us_per_call": round(sum(x - med for x in slow) / n * 1e6, 3)}
+    if pair_of:
+        byp = {}
+        for x, g in zip(calls, pair_of):
+            byp.setdefault(g, []).append(x)
+        out["median_us_by_pair"] = [round(sorted(byp[g])[len(byp[g]) // 2] * 1e6, 2) for g in sorted(byp)]
+    return out
 
 
 def park_until_rank0(use_pg: bool, world: int, rank: int, dist, key: str, timeout_s: float = 600.0):
@@ -859,7 +870,8 @@ def main():
     dt, dt_fresh, fresh_writes, step, dt_py = sync_loops(m, lib, reduce_local, ptrs, count, args.steps,
                                                          args.warmup, sync, barrier, max_over_ranks, own, c_loop,
                                                          calls)
-    cstats = call_stats(calls, alg_bytes)
+    # timed call i is step W + i: operand pair (W + i) % NPAIRS
+    cstats = call_stats(calls, alg_bytes, [(args.warmup + i) % NPAIRS for i in range(len(calls))])
     direct_share = (lib.MPIR_Hip_direct_dispatches() - d_before) / ((3 if c_loop else 2) * (args.steps + args.warmup))
     value = alg_bytes * args.steps * world / dt / GIB
     # each rank's own figures beside the max-over-ranks `value`: a lagging GPU,
