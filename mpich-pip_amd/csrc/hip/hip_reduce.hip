@@ -770,8 +770,10 @@ bool cpu_agent(hsa_agent_t a) {
 // (hipHostMalloc: pinned, whose owning device orders the caller's null-stream
 // work before the read), RESERVED_ADDR, graphics interop -- and UNKNOWN, which
 // is pageable memory, memory registered with hipHostRegister (HIP registers it
-// without HSA's lock), but also managed memory (hipMallocManaged answered
-// RESERVED_ADDR on one box and UNKNOWN on the next: profiles/r05/).  For host
+// without HSA's lock), but also managed memory (hipMallocManaged answers
+// RESERVED_ADDR in a plain C process, UNKNOWN in a Python process that also
+// loaded torch's bundled ROCm runtime: profiles/r05/classify_cost.log,
+// classify_diag.log).  For host
 // pages -- UNKNOWN, LOCKED, or an allocation owned by a CPU agent -- HIP's host
 // verdicts (pageable, pinned) are kept per thread, keyed by the 4 KiB page: the
 // next call on the same host buffers costs the HSA query and a lookup.  Only
