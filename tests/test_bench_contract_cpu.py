@@ -1,4 +1,4 @@
-"""The committed bench line (profiles/r05/bench_r05c.log, measured on MI355X) against
+"""The committed bench line (profiles/r05/bench_r05h.log, measured on MI355X) against
 the driver's contract and against itself: BASELINE.json's metric, the
 required keys, value = algorithmic bytes x N / time, roofline.frac =
 achieved / peak with achieved = 805,306,368 B / mean launch time, and the
@@ -10,7 +10,7 @@ import os
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LINE = os.path.join(ROOT, "profiles", "r05", "bench_r05c.log")
+LINE = os.path.join(ROOT, "profiles", "r05", "bench_r05h.log")
 GIB = float(1 << 30)
 
 
@@ -101,3 +101,7 @@ def test_call_distribution(line):
     assert d["kernel_us_for_call_at_0.80"] == pytest.approx(alg / (0.8 * 8.0e12) * 1e6 - d["fixed_us"], abs=0.02)
     pr = line["per_rank"][0]
     assert pr["call_median_us"] == cd["median_us"] and pr["call_p10_p90_us"] == [cd["p10_us"], cd["p90_us"]]
+    # the slow calls (> median + 4 us) and the per-pair medians (4 rotating pairs)
+    assert 0.0 <= cd["slow_share"] <= 1.0 and cd["slow_excess_us_per_call"] >= 0.0
+    assert len(cd["median_us_by_pair"]) == 4
+    assert min(cd["median_us_by_pair"]) <= cd["median_us"] <= max(cd["median_us_by_pair"]) + 1e-6
