@@ -877,7 +877,8 @@ def main():
     # each rank's own figures beside the max-over-ranks `value`: a lagging GPU,
     # or a rank whose calls left the direct path, shows here
     rows = gather_rows([float(rank), float(dev), own[0], own[1], float(lib.MPIR_Hip_direct_state(dev)),
-                        direct_share, cstats["median_us"], cstats["p10_us"], cstats["p90_us"]], world, dist,
+                        direct_share, cstats["median_us"], cstats["p10_us"], cstats["p90_us"],
+                        cstats["slow_share"]], world, dist,
                        "cpu" if pg_backend == "gloo" else "cuda")
 
     def rate(seconds):
@@ -929,7 +930,8 @@ def main():
                       "frac_of_hbm_peak": round(alg_bytes * args.steps / r[2] / HBM_PEAK_BPS, 4),
                       "fresh_args_seconds": round(r[3], 6), "direct_state": int(r[4]),
                       "direct_share": round(r[5], 4),
-                      "call_median_us": r[6], "call_p10_p90_us": [r[7], r[8]]} for r in rows],
+                      "call_median_us": r[6], "call_p10_p90_us": [r[7], r[8]], "slow_share": r[9]}
+                     for r in rows],
         # rank 0's K timed calls, each on its own (clock stamps in the C loop)
         "call_distribution": dict(cstats, source="CLOCK_MONOTONIC after each call of the timed C loop (rank 0)"
                                   if c_loop else "perf_counter after each step of the timed loop (rank 0)"),
