@@ -108,6 +108,7 @@ def main():
     row("read reqs 32 B share", lambda k: c(k, "TCC_EA0_RDREQ_32B_sum") / c(k, "TCC_EA0_RDREQ_sum"))
     row("RD DRAM credit stall / RD req", lambda k: c(k, "TCC_EA0_RDREQ_DRAM_CREDIT_STALL_sum") / c(k, "TCC_EA0_RDREQ_sum"))
     row("WR DRAM credit stall / WR req", lambda k: c(k, "TCC_EA0_WRREQ_DRAM_CREDIT_STALL_sum") / c(k, "TCC_EA0_WRREQ_sum"))
+    row("WR EA stall / WR req", lambda k: c(k, "TCC_EA0_WRREQ_STALL_sum") / c(k, "TCC_EA0_WRREQ_sum"))
     row("RD level / RD req (cycles)", lambda k: c(k, "TCC_EA0_RDREQ_LEVEL_sum") / c(k, "TCC_EA0_RDREQ_sum"), "{:14.1f}")
     row("WR level / WR req (cycles)", lambda k: c(k, "TCC_EA0_WRREQ_LEVEL_sum") / c(k, "TCC_EA0_WRREQ_sum"), "{:14.1f}")
     row("RD DRAM reqs / RD reqs", lambda k: c(k, "TCC_EA0_RDREQ_DRAM_sum") / c(k, "TCC_EA0_RDREQ_sum"))
