@@ -234,7 +234,10 @@ def run_collectives_child(rank: int, world: int, local: int, barrier, timeout: f
     """Configs 4-5 (Allreduce fp32 256 MiB, Reduce_scatter_block fp16 1 GiB) in a
     child process per rank with its own RCCL communicator, so a failure there
     cannot take this process's measurement down: the child is killed after
-    `timeout` seconds and the error is reported instead."""
+    `timeout` seconds and the error is reported instead.  main() runs it before
+    this process touches the GPU, so the child never shares the card with its
+    own live rank; the children meet over their own TCPStore, and `barrier`
+    (a no-op there) only lines the ranks up when they have a group already."""
     import subprocess
     barrier()
     env = dict(os.environ, RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(local),
@@ -774,6 +777,12 @@ def main():
     ring_variant = None
     if world == 1 and not args.no_extras and not args.no_variants:
         ring_variant = run_variant_child(args)
+    # configs 4-5 (RCCL collectives) in a child per rank, also before this
+    # process starts the GPU: one process per rank holds a GPU at any time
+    # (a child beside a live rank would double the processes on each card)
+    coll = None
+    if args.collectives == "on" or (args.collectives == "auto" and world > 1 and not args.no_extras):
+        coll = run_collectives_child(rank, world, local, lambda: None)
     import mpich_pip_amd as m
     # the library first, as a program linked against libmpi loads it before
     # main(): the process is still single-threaded (no numpy / torch yet), so the
@@ -1092,10 +1101,8 @@ def main():
                                         "the copy threads (SURVEY 8b: both operands host -> CPU)"}
         del ha, hb, pa, pb
 
-    if args.collectives == "on" or (args.collectives == "auto" and world > 1 and not args.no_extras):
-        coll = run_collectives_child(rank, world, dev, barrier)
-        if rank == 0:
-            out["collectives"] = coll
+    if coll is not None and rank == 0:
+        out["collectives"] = coll
 
     # the CPU baseline on rank 0 at every N, after the GPU work, the other
     # ranks parked on a blocking store read (no spinning core beside it)

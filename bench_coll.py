@@ -151,7 +151,10 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
+    # local % count: bench.py's one-GPU rehearsal (BENCH_TEST_SHARE_GPU) puts
+    # every rank on the one card, where RCCL refuses the communicator and the
+    # error is what bench.py reports
+    torch.cuda.set_device(local % max(1, torch.cuda.device_count()))
     lib = m.load()
     lib.MPIX_Reduce_local_set_errhandler(m.MPI_ERRORS_RETURN)
 
