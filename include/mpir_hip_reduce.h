@@ -87,6 +87,12 @@ size_t MPIR_Hip_elem_size(int elem);
 int MPIR_Hip_has_kernel(int op, int elem);
 /* 1 if p is device-accessible memory (hipMalloc / managed), 0 otherwise */
 int MPIR_Hip_is_device_ptr(const void *p);
+/* how a reduction of `bytes` sees p: 0 pageable host memory, 1 device memory,
+ * 2 pinned host memory (hipHostMalloc / hipHostRegister).  A call within the
+ * mixed slot's and the host combine's limits (MPIR_Hip_mixed_max_bytes,
+ * MPIR_Hip_host_max_bytes) may take this thread's kept verdict for p's page; a
+ * larger one asks HIP again (pointer classification) */
+int MPIR_Hip_pointer_kind(const void *p, uint64_t bytes);
 /* synchronous copy between any two pointers (device/host in any mix) */
 int MPIR_Hip_memcpy(void *dst, const void *src, size_t bytes);
 /* last runtime error text for this thread ("" if none) */

@@ -778,10 +778,17 @@ bool cpu_agent(hsa_agent_t a) {
 // verdicts (pageable, pinned) are kept per thread, keyed by the 4 KiB page: the
 // next call on the same host buffers costs the HSA query and a lookup.  Only
 // host verdicts are kept, and only looked up behind one of those answers, so a
-// stale one is harmless: a page that later becomes a GPU allocation answers HSA
-// as the GPU's, and one that becomes managed memory is host-accessible (the
-// host path reads it correctly); a device verdict is never reused.
-Loc classify(const void *p, int *dev) {
+// stale one never sends host memory to a kernel: a page that later becomes a GPU
+// allocation answers HSA as the GPU's, and one that becomes managed memory is
+// host-accessible (the host path reads it correctly); a device verdict is never
+// reused.  What a stale host verdict can change is the host path's choice, since
+// HSA reports pages pinned by hipHostRegister as UNKNOWN before and after: a
+// page registered after its verdict was kept would be bounced like pageable
+// memory instead of DMA'd.  So only calls that cannot reach the staged pipeline
+// (`reuse`, verdict_reusable below: within both the mixed slot's and the host
+// combine's limits, where pinned and pageable differ only in the null-stream
+// ordering) take a kept verdict; a larger call asks HIP again and refreshes it.
+Loc classify(const void *p, int *dev, bool reuse = true) {
     if (!gpu_runtime_started()) return LOC_HOST;
     hsa_amd_pointer_info_t info;
     info.size = sizeof info;
@@ -800,7 +807,7 @@ Loc classify(const void *p, int *dev) {
     if (!host_page) return classify_hip(p, dev);
     const uintptr_t page = reinterpret_cast<uintptr_t>(p) >> 12;
     HostVerdict &v = ctx().verdict[(page ^ (page >> 7)) & (kVerdicts - 1)];
-    if (v.page == page) {
+    if (reuse && v.page == page) {
         *dev = v.dev;
         return (Loc)v.loc;
     }
@@ -809,9 +816,13 @@ Loc classify(const void *p, int *dev) {
         v.page = page;
         v.loc = l;
         v.dev = l == LOC_PINNED ? *dev : 0;
+    } else if (v.page == page) {
+        v.page = ~(uintptr_t)0;
     }
     return l;
 }
+
+bool verdict_reusable(uint64_t bytes) { return bytes <= mixed_max_bytes() && bytes <= host_max_bytes(); }
 
 // devices visible to this process (0 on a CPU-only rank: host operands are
 // still combined there, as the reference's loop runs anywhere)
@@ -1032,6 +1043,11 @@ int MPIR_Hip_thread_contexts(void) {
 
 int MPIR_Hip_device_count(void) { return device_count(); }
 
+int MPIR_Hip_pointer_kind(const void *p, uint64_t bytes) {
+    int dev = 0;
+    return classify(p, &dev, verdict_reusable(bytes));
+}
+
 int MPIR_Hip_is_device_ptr(const void *p) {
     int dev = 0;
     return classify(p, &dev) == LOC_DEVICE;
@@ -1120,8 +1136,9 @@ int MPIR_Hip_reduce(const void *inbuf, void *inoutbuf, uint64_t count, int op, i
     ctx().err[0] = 0;
     launch_fn fn = g_table[op][elem].fn;
     int din = -1, dio = -1;
-    const Loc lin = classify(inbuf, &din);
-    const Loc lio = classify(inoutbuf, &dio);
+    const bool reuse = verdict_reusable(count * esz);
+    const Loc lin = classify(inbuf, &din, reuse);
+    const Loc lio = classify(inoutbuf, &dio, reuse);
 
     // ---- fast path: both operands device-resident on one device ----------
     if (lin == LOC_DEVICE && lio == LOC_DEVICE && din == dio)

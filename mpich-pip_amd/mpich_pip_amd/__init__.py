@@ -118,7 +118,7 @@ EXPORTED_SYMBOLS = [
     "MPIX_Scan_hip", "MPIX_Exscan_hip",
     # the HIP shim (include/mpir_hip_reduce.h)
     "MPIR_Hip_reduce", "MPIR_Hip_elem_size", "MPIR_Hip_has_kernel", "MPIR_Hip_is_device_ptr",
-    "MPIR_Hip_memcpy", "MPIR_Hip_error_string", "MPIR_Hip_device_count", "MPIR_Hip_thread_contexts",
+    "MPIR_Hip_pointer_kind", "MPIR_Hip_memcpy", "MPIR_Hip_error_string", "MPIR_Hip_device_count", "MPIR_Hip_thread_contexts",
     "MPIR_Hip_host_max_bytes", "MPIR_Hip_set_host_max_bytes", "MPIR_Hip_mixed_max_bytes", "MPIR_Hip_direct_dispatches", "MPIR_Hip_direct_profile",
     "MPIR_Hip_direct_last_kernel_ns", "MPIR_Hip_direct_state", "MPIR_Hip_direct_busy_skips",
     "MPIR_Hip_direct_last_split", "MPIR_Hip_direct_kernarg_writes",
@@ -204,6 +204,8 @@ def load(path: str | None = None) -> ctypes.CDLL:
     lib.MPIR_Hip_direct_last_split.argtypes = [ctypes.POINTER(ctypes.c_uint64)]
     lib.MPIR_Hip_direct_last_split.restype = None
     lib.MPIR_Hip_error_string.restype = ctypes.c_char_p
+    lib.MPIR_Hip_pointer_kind.argtypes = [vp, ctypes.c_uint64]
+    lib.MPIR_Hip_pointer_kind.restype = i32
     for name in [n for n in EXPORTED_SYMBOLS if n.endswith("_check_dtype")]:
         f = getattr(lib, name)
         f.argtypes = [i32]

@@ -182,6 +182,7 @@ class Kinds:
 KINDS = [("hipMalloc", "device", 1), ("hipMallocAsync", "pool", 1), ("VMM", "vmm", 1),
          ("hipMallocManaged", "managed", 1), ("hipHostMalloc", "pinned", 0),
          ("hipHostRegister", "registered", 0), ("pageable", "pageable", 0)]
+KIND_CLASS = {"device": 1, "pool": 1, "vmm": 1, "managed": 1, "pinned": 2, "registered": 2, "pageable": 0}
 
 
 def _put(hip, dst, arr):
@@ -221,6 +222,8 @@ def _case(mpi, orc, hip, name, maker, is_dev):
         pre = _diag(hip, x)
         got = lib.MPIR_Hip_is_device_ptr(ctypes.c_void_p(x))
         assert got == is_dev, (name, pre, _diag(hip, x), lib.MPIR_Hip_is_device_ptr(ctypes.c_void_p(x)))
+        # the class a 1 MiB call sees: 0 pageable, 1 device, 2 pinned
+        assert lib.MPIR_Hip_pointer_kind(ctypes.c_void_p(x), NB) == KIND_CLASS[maker], (name, pre)
         rng = np.random.default_rng(sum(map(ord, name)))
         a = rng.uniform(-1, 1, N).astype(np.float32)
         b = rng.uniform(-1, 1, N).astype(np.float32)
@@ -236,3 +239,61 @@ def _case(mpi, orc, hip, name, maker, is_dev):
             assert np.array_equal(got.view(np.uint32), want.view(np.uint32)), (name, pin == x, pio == x)
     finally:
         ks.close()
+
+
+def test_registration_after_kept_verdict(mpi, orc, hip):
+    """One thread, one page: a pageable buffer reduced small (its verdict kept),
+    then registered with hipHostRegister -- which HSA still reports as UNKNOWN --
+    and reduced large: the large call asks HIP again and sees it pinned; after
+    hipHostUnregister a large call sees it pageable again.  Every reduction
+    bit-exact (hip_reduce.hip classify, `reuse`)."""
+    lib = mpi.load()
+    err = []
+
+    def body():
+        try:
+            buf = np.zeros(NB + 8192, np.uint8)
+            addr = (buf.ctypes.data + 4095) & ~4095
+            x = np.frombuffer((ctypes.c_char * NB).from_address(addr), np.float32)
+            d = Kinds(hip)
+            dv = d.device()
+            rng = np.random.default_rng(11)
+            a = rng.uniform(-1, 1, N).astype(np.float32)
+            b = rng.uniform(-1, 1, N).astype(np.float32)
+
+            def check(n):
+                # inbuf = the host page, inoutbuf = a device buffer
+                x[:n] = b[:n]
+                _put(hip, dv, a)
+                rc = lib.MPI_Reduce_local(ctypes.c_void_p(addr), ctypes.c_void_p(dv), n, mpi.MPI_FLOAT, mpi.MPI_SUM)
+                assert rc == 0, mpi.error_string(rc)
+                want = a[:n].copy()
+                assert orc.reduce_local(b[:n].copy(), want, n, mpi.MPI_FLOAT, mpi.MPI_SUM) == 0
+                got = _get(hip, dv)[:n]
+                assert np.array_equal(got.view(np.uint32), want.view(np.uint32)), n
+
+            try:
+                check(16)
+                assert lib.MPIR_Hip_pointer_kind(ctypes.c_void_p(addr), 64) == 0
+                _ok(hip.hipHostRegister(ctypes.c_void_p(addr), ctypes.c_size_t(NB), 0), "hipHostRegister")
+                try:
+                    # a small call may keep the pageable verdict (only the null-stream ordering differs)
+                    assert lib.MPIR_Hip_pointer_kind(ctypes.c_void_p(addr), 64) in (0, 2)
+                    assert lib.MPIR_Hip_pointer_kind(ctypes.c_void_p(addr), NB) == 2, _diag(hip, addr)
+                    assert lib.MPIR_Hip_pointer_kind(ctypes.c_void_p(addr), 64) == 2      # refreshed
+                    check(N)
+                    check(16)
+                finally:
+                    _ok(hip.hipHostUnregister(ctypes.c_void_p(addr)), "hipHostUnregister")
+                assert lib.MPIR_Hip_pointer_kind(ctypes.c_void_p(addr), NB) == 0, _diag(hip, addr)
+                check(N)
+            finally:
+                d.close()
+        except BaseException as e:      # noqa: BLE001
+            err.append(e)
+    t = threading.Thread(target=body)
+    t.start()
+    t.join(120)
+    assert not t.is_alive(), "case hung"
+    if err:
+        raise err[0]
