@@ -259,15 +259,29 @@ def run_collectives_child(rank: int, world: int, local: int, barrier, timeout: f
 
 
 def time_loop(run, k: int, w: int, sync, barrier, max_over_ranks, own: list | None = None,
-              calls: list | None = None) -> float:
+              calls: list | None = None, gap: list | None = None) -> float:
     """time_steps for a C loop: run(start, n[, stamps]) makes steps start ..
     start + n - 1 back to back; W untimed steps, then exactly K timed ones
     between barrier + device sync, max over ranks.  `calls`, if given, receives
     the K timed calls' own durations (seconds), from the loop's per-call clock
-    stamps."""
-    run(0, w)
-    sync()
-    barrier()
+    stamps; `gap`, if given, the host time between the last warm-up call's
+    return and the first timed call (seconds, same clock).
+
+    The last warm-up step runs after the barrier (BENCH_WARMUP_ORDER=before:
+    all W before it): the command processor drops into a deeper idle state
+    after 50-100 us without a doorbell (DESIGN.md "Idle gaps"), and a barrier
+    over a process group takes longer than that, so without it the first timed
+    call would pay a wake-up that back-to-back calls never see."""
+    late = w > 0 and os.environ.get("BENCH_WARMUP_ORDER", "late") != "before"
+    run(0, w - 1 if late else w)
+    if late:
+        sync()
+        barrier()
+        run(w - 1, 1)
+    warm_end = time.monotonic_ns()         # CLOCK_MONOTONIC, the C loop's clock
+    if not late:
+        sync()
+        barrier()
     sync()
     stamps = None
     if calls is not None:
@@ -285,6 +299,8 @@ def time_loop(run, k: int, w: int, sync, barrier, max_over_ranks, own: list | No
         own.append(t1 - t0)
     if calls is not None:
         calls.extend((np.diff(stamps) * 1e-9).tolist())
+        if gap is not None:
+            gap.append((int(stamps[0]) - warm_end) * 1e-9)
     return max_over_ranks(t1 - t0)
 
 
@@ -332,7 +348,7 @@ def park_until_rank0(use_pg: bool, world: int, rank: int, dist, key: str, timeou
 
 
 def sync_loops(m, lib, reduce_local, ptrs, count, k: int, w: int, sync, barrier, max_over_ranks,
-               own: list | None = None, c_loop=None, calls: list | None = None):
+               own: list | None = None, c_loop=None, calls: list | None = None, gap: list | None = None):
     """The headline loop (NPAIRS pairs rotated: every call after the first
     NPAIRS repeats its kernel arguments, which the direct dispatch's kernarg
     cache then holds) and the same loop with fresh arguments on every call: the
@@ -367,7 +383,7 @@ def sync_loops(m, lib, reduce_local, ptrs, count, k: int, w: int, sync, barrier,
         return run
     dt_py = None
     if c_loop is not None:
-        dt = time_loop(runner(call_args), k, w, sync, barrier, max_over_ranks, own, calls)
+        dt = time_loop(runner(call_args), k, w, sync, barrier, max_over_ranks, own, calls, gap)
         kw0 = lib.MPIR_Hip_direct_kernarg_writes()
         dtf = time_loop(runner(fresh_args), k, w, sync, barrier, max_over_ranks, own)
         writes = (lib.MPIR_Hip_direct_kernarg_writes() - kw0) / (k + w)
@@ -874,13 +890,20 @@ def main():
         binding = "C loop of the compiled binding (csrc/py/fastcall.c reduce_local_loop)"
     except ImportError:     # extension not built: the same C entry point through ctypes
         reduce_local, c_loop, binding = lib.MPI_Reduce_local, None, "ctypes"
-    own, calls = [], []
+    own, calls, gap = [], [], []
     d_before = lib.MPIR_Hip_direct_dispatches()
     dt, dt_fresh, fresh_writes, step, dt_py = sync_loops(m, lib, reduce_local, ptrs, count, args.steps,
                                                          args.warmup, sync, barrier, max_over_ranks, own, c_loop,
-                                                         calls)
+                                                         calls, gap)
     # timed call i is step W + i: operand pair (W + i) % NPAIRS
     cstats = call_stats(calls, alg_bytes, [(args.warmup + i) % NPAIRS for i in range(len(calls))])
+    if calls:
+        # the first timed call follows the barrier and device syncs: the host
+        # gap before it, and the call itself (the CP idles deeper after 50-100 us
+        # without a doorbell, DESIGN.md "Idle gaps")
+        cstats["first_call_us"] = round(calls[0] * 1e6, 2)
+        if gap:
+            cstats["idle_gap_before_first_us"] = round(gap[0] * 1e6, 1)
     direct_share = (lib.MPIR_Hip_direct_dispatches() - d_before) / ((3 if c_loop else 2) * (args.steps + args.warmup))
     value = alg_bytes * args.steps * world / dt / GIB
     # each rank's own figures beside the max-over-ranks `value`: a lagging GPU,
