@@ -949,7 +949,11 @@ def main():
             "kernel_arguments": "%d rotating pairs: every call after the first %d repeats its arguments (kernarg "
                                 "cache hit); sync_variants.fresh_args misses on every call" % (NPAIRS, NPAIRS),
             "caller": "K synchronous MPI_Reduce_local calls back to back from C (" + binding + "); "
-                      "sync_variants.python_loop steps the same calls from Python"},
+                      "sync_variants.python_loop steps the same calls from Python",
+            "warmup": "W untimed steps, the last of them after the barrier (BENCH_WARMUP_ORDER="
+                      + os.environ.get("BENCH_WARMUP_ORDER", "late") + "), then a device sync and the K timed "
+                      "steps: the first timed call does not pay the command processor's idle wake-up "
+                      "(call_distribution.first_call_us, idle_gap_before_first_us)"},
         # the synchronous call per GPU (launch + completion included) against the HBM peak
         "per_gpu": {"GiBps": round(value / world, 1),
                     "frac_of_hbm_peak": round(value / world * GIB / HBM_PEAK_BPS, 4),
