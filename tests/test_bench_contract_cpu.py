@@ -1,4 +1,4 @@
-"""The committed bench line (profiles/r05/bench_r05h.log, measured on MI355X) against
+"""The committed bench line (profiles/r05/bench_r05r.log, measured on MI355X) against
 the driver's contract and against itself: BASELINE.json's metric, the
 required keys, value = algorithmic bytes x N / time, roofline.frac =
 achieved / peak with achieved = 805,306,368 B / mean launch time, and the
@@ -10,7 +10,7 @@ import os
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LINE = os.path.join(ROOT, "profiles", "r05", "bench_r05h.log")
+LINE = os.path.join(ROOT, "profiles", "r05", "bench_r05r.log")
 GIB = float(1 << 30)
 
 
@@ -105,3 +105,8 @@ def test_call_distribution(line):
     assert 0.0 <= cd["slow_share"] <= 1.0 and cd["slow_excess_us_per_call"] >= 0.0
     assert len(cd["median_us_by_pair"]) == 4
     assert min(cd["median_us_by_pair"]) <= cd["median_us"] <= max(cd["median_us_by_pair"]) + 1e-6
+    # the first timed call and the host gap before it: the last warm-up step runs
+    # after the barrier, so the gap is a device sync, not a barrier
+    assert cd["min_us"] <= cd["first_call_us"] <= cd["max_us"]
+    assert 0.0 < cd["idle_gap_before_first_us"] < 50.0
+    assert "after the barrier" in line["value_conditions"]["warmup"]
