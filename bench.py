@@ -11,7 +11,10 @@ barrier and the max-over-ranks of the elapsed time.
 A step is one MPI_Reduce_local(inbuf, inoutbuf, 67108864, MPI_FLOAT, MPI_SUM)
 call through the C ABI -- the public, synchronous entry point (it returns
 with the result complete).  Timed: exactly K steps between barrier +
-torch.cuda.synchronize() on both sides, after W untimed warm-up steps.
+torch.cuda.synchronize() on both sides, after W untimed warm-up steps, the
+last of which runs after the opening barrier so the first timed call does not
+pay the command processor's idle wake-up (BENCH_WARMUP_ORDER=before: all W
+before the barrier).
     value = 3 * 256 MiB * K * N / max_rank_seconds / 2^30   (GiB/s, algorithmic bytes:
             read inbuf, read inoutbuf, write inoutbuf -- SURVEY.md §8d)
 
@@ -53,8 +56,9 @@ Extra fields (rank 0):
                 NUMA-local operands, a bounded sample, per socket; rank 0 at every N,
                 after the GPU work, the other ranks parked on a blocking store read.
   call_distribution  rank 0's K timed calls one by one (median, p10 / p90,
-                mean, min / max; per-call clock stamps in the C loop), and the
-                call split into kernel + fixed cost.
+                mean, min / max; per-call clock stamps in the C loop), the call
+                split into kernel + fixed cost, the first timed call and the host
+                gap before it.
 """
 from __future__ import annotations
 
