@@ -48,7 +48,7 @@ uint64_t direct_kernarg_writes();
 uint32_t direct_test_write_delay_us(uint32_t us);
 void direct_test_fail_probe();
 Entry g_table[MPIR_HIP_NOPS][MPIR_HIP_NELEMS];
-multi_fn g_multi[MPIR_HIP_NOPS][MPIR_HIP_NELEMS][2][3];
+multi_fn g_multi[MPIR_HIP_NOPS][MPIR_HIP_NELEMS][2][kMultiMaxP - 1];
 
 // Results of at most this many bytes are stored sc1 (into the Infinity Cache)
 // rather than nt: MPIR_CVAR_REDUCE_LOCAL_KEEP_MB (0 = every store nt), default
@@ -1088,19 +1088,19 @@ int MPIR_Hip_combine(const void *const *inbufs, int n, void *outbuf, uint64_t co
             if (outbuf != inbufs[n - 1])
                 e = hipMemcpyAsync(outbuf, inbufs[n - 1], count * esz, hipMemcpyDeviceToDevice, s);
         } else if (order == MPIR_HIP_ORDER_TREE && fused && n <= 8) {
-            e = g_multi[op][elem][0][n == 2 ? 0 : (n == 4 ? 1 : 2)](inbufs, outbuf, count, s);
+            e = g_multi[op][elem][0][n - 2](inbufs, outbuf, count, s);
         } else if (order == MPIR_HIP_ORDER_CHAIN && fused) {
-            // CHAIN: acc = y0; fold y1..y_{n-1} in order.  Greedy chunks of
-            // P = 8/4/2 operands, each chunk's first operand the running acc.
+            // CHAIN: acc = y0; fold y1..y_{n-1} in order, one pass for n <= 8;
+            // beyond, chunks of up to 8 operands, each chunk's first operand the
+            // running acc
             const void *acc = inbufs[0];
             int i = 1;
             while (e == hipSuccess && i < n) {
-                const int left = n - i;
-                const int P = left >= 7 ? 8 : (left >= 3 ? 4 : 2);
-                const void *ops[8];
+                const int P = std::min(kMultiMaxP, n - i + 1);
+                const void *ops[kMultiMaxP];
                 ops[0] = acc;
                 for (int j = 1; j < P; ++j) ops[j] = inbufs[i + j - 1];
-                e = g_multi[op][elem][1][P == 2 ? 0 : (P == 4 ? 1 : 2)](ops, outbuf, count, s);
+                e = g_multi[op][elem][1][P - 2](ops, outbuf, count, s);
                 i += P - 1;
                 acc = outbuf;
             }

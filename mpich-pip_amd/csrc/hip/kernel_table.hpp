@@ -8,8 +8,11 @@
 // g_table[op][elem].host: the same combine as a host loop over the same
 //                        functors (reduce_ops.hpp), for small operands that
 //                        both live in host memory (MPIR_Hip_reduce);
-// g_multi[op][elem][order][P = 2, 4, 8]: the fused schedule combines
-//                        (k_combine_multi) for the ops the collectives use most.
+// g_multi[op][elem][order][P - 2]: the fused schedule combines
+//                        (k_combine_multi) for the ops the collectives use most:
+//                        TREE folds of P = 2, 4, 8 operands, CHAIN folds of every
+//                        P from 2 to 8 (a pairwise chain over p ranks is one pass
+//                        for any p <= 8).
 // Storage lives in hip_reduce.hip (zero-initialised); the reg_*.hip units fill
 // it from static constructors, one unit per op family so they compile in
 // parallel.  The ops a type admits follow src/include/mpir_op_util.h:263-364.
@@ -100,7 +103,8 @@ void host_loop(const void *in, void *io, uint64_t n) {
     }
 }
 extern Entry g_table[MPIR_HIP_NOPS][MPIR_HIP_NELEMS];
-extern multi_fn g_multi[MPIR_HIP_NOPS][MPIR_HIP_NELEMS][2][3];
+constexpr int kMultiMaxP = 8;
+extern multi_fn g_multi[MPIR_HIP_NOPS][MPIR_HIP_NELEMS][2][kMultiMaxP - 1];
 
 template <class Op, class T>
 void reg(int op, int elem) {
@@ -119,12 +123,16 @@ void reg_wide(int op, int elem) {
 }
 template <class Op, class T>
 void reg_multi(int op, int elem) {
-    g_multi[op][elem][0][0] = &launch_combine_p<Op, T, 2, true>;
-    g_multi[op][elem][0][1] = &launch_combine_p<Op, T, 4, true>;
-    g_multi[op][elem][0][2] = &launch_combine_p<Op, T, 8, true>;
-    g_multi[op][elem][1][0] = &launch_combine_p<Op, T, 2, false>;
-    g_multi[op][elem][1][1] = &launch_combine_p<Op, T, 4, false>;
-    g_multi[op][elem][1][2] = &launch_combine_p<Op, T, 8, false>;
+    g_multi[op][elem][0][2 - 2] = &launch_combine_p<Op, T, 2, true>;
+    g_multi[op][elem][0][4 - 2] = &launch_combine_p<Op, T, 4, true>;
+    g_multi[op][elem][0][8 - 2] = &launch_combine_p<Op, T, 8, true>;
+    g_multi[op][elem][1][2 - 2] = &launch_combine_p<Op, T, 2, false>;
+    g_multi[op][elem][1][3 - 2] = &launch_combine_p<Op, T, 3, false>;
+    g_multi[op][elem][1][4 - 2] = &launch_combine_p<Op, T, 4, false>;
+    g_multi[op][elem][1][5 - 2] = &launch_combine_p<Op, T, 5, false>;
+    g_multi[op][elem][1][6 - 2] = &launch_combine_p<Op, T, 6, false>;
+    g_multi[op][elem][1][7 - 2] = &launch_combine_p<Op, T, 7, false>;
+    g_multi[op][elem][1][8 - 2] = &launch_combine_p<Op, T, 8, false>;
 }
 
 }  // namespace mpir_hip

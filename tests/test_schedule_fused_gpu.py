@@ -249,16 +249,18 @@ EVERY = [(op, t) for op in T.OPS for t in T.ALL_TYPES if T.compute_ok(op, t)]
 @pytest.mark.parametrize("op,t", EVERY, ids=[f"{o}-{t}" for o, t in EVERY])
 def test_every_pair_fused_matches_stepwise_fold(mpi, orc, cuda, op, t):
     """Every (op, type) the reference computes, through MPIX_Reduce_local_multi:
-    TREE of 8 (one fused pass), CHAIN of 8 (one pass) and CHAIN of 5 (greedy
-    4 + 2 passes, the second reading the first's output) against the same
-    fold done one oracle MPIR_Reduce_local step at a time.  Operands with
+    TREE of 8 (one fused pass), CHAIN of 3, 5, 6, 7 and 8 (one pass each: the
+    pairwise chain of every rank count up to 8) and CHAIN of 11 (a pass of 8,
+    then one of 4 reading the first's output) against the same fold done one
+    oracle MPIR_Reduce_local step at a time.  Operands with
     specials (NaN, +-0, inf, denormals, extremes); the second round starts
     every buffer one element past 256 B alignment so the fused kernel's head
     and tail elements run too."""
     torch = cuda
     esz = T.elem_size(t)
     dt, o = mpi.DATATYPES[t], mpi.OPS[op]
-    for k, (n, order) in enumerate(((8, "TREE"), (8, "CHAIN"), (5, "CHAIN"))):
+    for k, (n, order) in enumerate(((8, "TREE"), (8, "CHAIN"), (5, "CHAIN"), (3, "CHAIN"), (6, "CHAIN"),
+                                    (7, "CHAIN"), (11, "CHAIN"))):
         for off in (0, esz):
             count = 3000 + 7 * n + k
             rng = np.random.default_rng(1000 * n + k + off)
