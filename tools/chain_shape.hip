@@ -1,0 +1,136 @@
+// chain_shape.hip -- workgroup shape and LDS cap of the fused CHAIN folds of
+// 3, 5, 6 and 7 operands (round 5: the library runs P = 5-7 in P = 8's shape,
+// 1024 threads x 1 vector under a 96 KiB cap = one workgroup per CU, and P = 3
+// in P = 4's, 256 threads x 4 vectors under a 53 KiB cap = three per CU).
+//
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off \
+//         -Impich-pip_amd/csrc/hip -o tools/chain_shape tools/chain_shape.hip
+//   tools/chain_shape [rounds = 9]
+//
+// fp16 SUM CHAIN over p blocks of 1 GiB / p (config 5's sendbuf at p ranks),
+// two operand sets alternated, HIP events over batches of 10 back-to-back
+// launches, shapes shuffled per round, first round dropped; every shape's
+// output compared bit for bit with the library shape's.
+#include <hip/hip_runtime.h>
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <random>
+#include <vector>
+
+#include "reduce_kernels.hpp"
+
+#define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { \
+    fprintf(stderr, "HIP %s at %s:%d\n", hipGetErrorString(e_), __FILE__, __LINE__); exit(2);} } while (0)
+
+namespace mpir_hip {
+uint64_t keep_bytes() { return kKeepBytes; }
+uint64_t keep_for(uint64_t vbytes) { return vbytes <= keep_bytes() ? vbytes : 0; }
+}
+using namespace mpir_hip;
+
+__global__ void k_fill(uint16_t *p, uint64_t n, uint32_t seed) {
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        uint32_t x = (uint32_t)i * 2654435761u ^ seed;
+        x ^= x << 13; x ^= x >> 17; x ^= x << 5;
+        p[i] = (uint16_t)(x & 0xBFFF);
+    }
+}
+
+struct Shape {
+    const char *name;
+    int th, u, lds;
+};
+
+template <int P, int U, int TH>
+void launch(const MultiArgs &a, int lds) {
+    const uint64_t tile = (uint64_t)TH * U * 16;
+    hipLaunchKernelGGL((k_combine_multi<OpSum, f16, P, false, U, TH>), dim3((unsigned)(a.vbytes / tile)), dim3(TH),
+                       lds, 0, a);
+}
+
+template <int P>
+void run(int rounds) {
+    CK(hipFuncSetAttribute((const void *)k_combine_multi<OpSum, f16, P, false, 1, 1024>,
+                           hipFuncAttributeMaxDynamicSharedMemorySize, 96 << 10));
+    CK(hipFuncSetAttribute((const void *)k_combine_multi<OpSum, f16, P, false, 4, kThreads>,
+                           hipFuncAttributeMaxDynamicSharedMemorySize, 96 << 10));
+    const Shape shapes[] = {{"1024 x 1, 96 KiB cap (1 / CU)", 1024, 1, 96 << 10}, {"1024 x 1, no cap (2 / CU)", 1024, 1, 0},
+                            {"256 x 4, 53 KiB cap (3 / CU)", 256, 4, 53 << 10}, {"256 x 4, 40 KiB cap (4 / CU)", 256, 4, 40 << 10},
+                            {"256 x 4, no cap", 256, 4, 0}};
+    constexpr int NS = 5;
+    const int lib = P >= 5 ? 0 : 2;
+    const uint64_t block = ((1ull << 30) / P) / 65536 * 65536;       // bytes, a multiple of both tiles
+    std::vector<char *> bufs(2 * P + 2);
+    for (auto &b : bufs) CK(hipMalloc(&b, block));
+    for (int i = 0; i < 2 * P; ++i) k_fill<<<2048, 256>>>((uint16_t *)bufs[i], block / 2, 0x99u + 13u * i);
+    CK(hipDeviceSynchronize());
+    auto args = [&](int set) {
+        MultiArgs a{};
+        for (int j = 0; j < P; ++j) a.in[j] = bufs[set * P + j];
+        a.out = bufs[2 * P + set];
+        a.vbytes = block;
+        a.keep = keep_for(block);
+        return a;
+    };
+    auto go = [&](int si, int set) {
+        const Shape &s = shapes[si];
+        if (s.th == 1024) launch<P, 1, 1024>(args(set), s.lds);
+        else launch<P, 4, kThreads>(args(set), s.lds);
+    };
+    std::vector<char> want(block), got(block);
+    int bad = 0;
+    go(lib, 0);
+    CK(hipDeviceSynchronize());
+    CK(hipMemcpy(want.data(), bufs[2 * P], block, hipMemcpyDeviceToHost));
+    for (int si = 0; si < NS; ++si) {
+        if (si == lib) continue;
+        CK(hipMemset(bufs[2 * P], 0, block));
+        go(si, 0);
+        CK(hipDeviceSynchronize());
+        CK(hipMemcpy(got.data(), bufs[2 * P], block, hipMemcpyDeviceToHost));
+        if (memcmp(got.data(), want.data(), block)) ++bad;
+    }
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    std::vector<double> us[NS];
+    std::mt19937 rng(P);
+    const int batch = 10;
+    int k = 0;
+    for (int r = 0; r < rounds; ++r) {
+        int order[NS];
+        for (int i = 0; i < NS; ++i) order[i] = i;
+        std::shuffle(order, order + NS, rng);
+        for (int si : order) {
+            go(si, k++ & 1);
+            CK(hipEventRecord(e0, 0));
+            for (int b = 0; b < batch; ++b) go(si, k++ & 1);
+            CK(hipEventRecord(e1, 0));
+            CK(hipEventSynchronize(e1));
+            float ms = 0;
+            CK(hipEventElapsedTime(&ms, e0, e1));
+            if (r) us[si].push_back(ms * 1e3 / batch);
+        }
+    }
+    printf("CHAIN%d fp16, %d x %.1f MiB: outputs %s\n", P, P, block / 1048576.0, bad ? "DIFFER" : "identical");
+    for (int si = 0; si < NS; ++si) {
+        std::sort(us[si].begin(), us[si].end());
+        const double med = us[si][us[si].size() / 2];
+        printf("  %-32s%s median %8.2f us  frac of 8 TB/s %.4f\n", shapes[si].name, si == lib ? " (library)" : "          ",
+               med, (P + 1.0) * block / (med * 1e-6) / 8e12);
+    }
+    CK(hipEventDestroy(e0));
+    CK(hipEventDestroy(e1));
+    for (auto b : bufs) CK(hipFree(b));
+}
+
+int main(int argc, char **argv) {
+    const int rounds = argc > 1 ? atoi(argv[1]) : 9;
+    run<3>(rounds);
+    run<5>(rounds);
+    run<6>(rounds);
+    run<7>(rounds);
+    return 0;
+}
