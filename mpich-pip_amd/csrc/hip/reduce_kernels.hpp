@@ -739,11 +739,13 @@ __global__ __launch_bounds__(kThreads) void k_combine_multi_elems(MultiArgs a, u
 #endif
 template <int P, int TH>
 constexpr int multi_cap_bytes() {
-    // P = 5-7 (CHAIN folds of non-power-of-two rank counts) take P = 8's shape
-    // and cap, P = 3 P = 4's
+    // P = 3 and 5-7 (CHAIN folds of non-power-of-two rank counts) take P = 4's
+    // shape and cap: 256 x 4 at three per CU ran 0.785-0.833 against 0.784-0.789
+    // in P = 8's shape (tools/chain_shape.hip, profiles/r05/chain_shape*.log),
+    // while P = 8 keeps its own (0.786 against 0.774)
     return !MPIR_MULTI_CAP_LDS ? 0
-           : (P >= 5 && TH == 1024) ? (96 << 10)
-           : ((P == 4 || P == 3) && TH == kThreads) ? (53 << 10) : 0;
+           : (P == 8 && TH == 1024) ? (96 << 10)
+           : (P >= 3 && P <= 7 && TH == kThreads) ? (53 << 10) : 0;
 }
 template <class Op, class T, int P, bool TREE, int U, int TH>
 size_t multi_lds_cap() {
@@ -872,8 +874,8 @@ hipError_t launch_combine_p(const void *const *ins, void *out_, uint64_t count, 
     // rocprofv3 trace, 32 MiB blocks (profiles/archive/r01s3_multi_shape_p24.log): P = 8 on
     // 1024-thread WGs (0.76-0.80 of peak); P = 4 with 4 vectors per lane 0.78-0.80
     // (2 vectors: 0.72-0.74); P = 2 with 4 vectors per lane 0.74-0.76
-    // (2, 4, 8 for TREE; every P of 2-8 for CHAIN: 5-7 in P = 8's shape, 3 in P = 4's)
-    return launch_combine_pu<Op, T, P, TREE, (P >= 5 ? 1 : 4), (P >= 5 ? 1024 : kThreads)>(ins, out_, count, s);
+    // (2, 4, 8 for TREE; every P of 2-8 for CHAIN: 3-7 in P = 4's shape)
+    return launch_combine_pu<Op, T, P, TREE, (P >= 8 ? 1 : 4), (P >= 8 ? 1024 : kThreads)>(ins, out_, count, s);
 }
 
 }  // namespace mpir_hip

@@ -60,7 +60,7 @@ void run(int rounds) {
                             {"256 x 4, 53 KiB cap (3 / CU)", 256, 4, 53 << 10}, {"256 x 4, 40 KiB cap (4 / CU)", 256, 4, 40 << 10},
                             {"256 x 4, no cap", 256, 4, 0}};
     constexpr int NS = 5;
-    const int lib = P >= 5 ? 0 : 2;
+    const int lib = P >= 5 ? 0 : 2;     // (as launched before this probe)
     const uint64_t block = ((1ull << 30) / P) / 65536 * 65536;       // bytes, a multiple of both tiles
     std::vector<char *> bufs(2 * P + 2);
     for (auto &b : bufs) CK(hipMalloc(&b, block));
@@ -132,5 +132,6 @@ int main(int argc, char **argv) {
     run<5>(rounds);
     run<6>(rounds);
     run<7>(rounds);
+    run<8>(rounds);     // config 5 at 8 ranks: the library's P = 8 shape against the others
     return 0;
 }
