@@ -632,6 +632,50 @@ def config2(m, lib, pairs, stream, k: int, w: int):
     return out
 
 
+def config4_combine(m, stream, k: int, w: int):
+    """Config 4's combine at one GPU: the fused TREE8 fold MPIX_Reduce_local_multi
+    runs in Allreduce's reference-order mode at 8 ranks (the recursive-halving
+    reduce-scatter, reduce_intra_reduce_scatter_gather.c:186-249): 8 blocks of
+    32 MiB fp32 (256 MiB / 8), ((y0+y1)+(y2+y3))+... into a 32 MiB output, the
+    blocks at the collective's staging stride (32 MiB + 4352 B), six sets
+    rotated (1.7 GiB a cycle, past the 256 MB Infinity Cache); HIP events on the
+    stream.  Fraction: 9 x 32 MiB over kernel time against 8.0 TB/s."""
+    import torch
+    blk = 8 * MIB                               # floats in 32 MiB
+    stride = blk + 4352 // 4                    # coll_hip.c stage_stride, in floats
+    g = torch.Generator(device="cuda").manual_seed(0xF32)
+    nsets = 6
+    sets = [torch.rand(8 * stride, device="cuda", generator=g) * 2 - 1 for _ in range(nsets)]
+    outs = [torch.empty(blk, device="cuda") for _ in range(nsets)]
+    torch.cuda.synchronize()
+    ops = [[s_.data_ptr() + 4 * j * stride for j in range(8)] for s_ in sets]
+
+    def launch(i):
+        rc = m.reduce_local_multi(ops[i % nsets], outs[i % nsets].data_ptr(), blk, m.MPI_FLOAT, m.MPI_SUM,
+                                  m.MPIX_ORDER_TREE, stream.cuda_stream)
+        assert rc == 0, m.error_string(rc)
+    with torch.cuda.stream(stream):
+        us = event_launch_us(launch, k, w, stream)
+        # back to back: one event pair around K launches (a ~50 us kernel loses
+        # several per cent to a per-launch event bracket)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for i in range(k):
+            launch(w + k + i)
+        e1.record(stream)
+    stream.synchronize()
+    us_b2b = e0.elapsed_time(e1) * 1e3 / k
+    alg = 9 * blk * 4
+    del sets, outs
+    torch.cuda.empty_cache()
+    return {"tree8": {"blocks": 8, "block_MiB": 32, "kernel": "k_combine_multi<OpSum, float, P=8, TREE> "
+                      "(256 x 4 shape below 128 MiB blocks)", "kernel_us": round(us_b2b, 2),
+                      "frac": round(alg / (us_b2b * 1e-6) / HBM_PEAK_BPS, 4),
+                      "timing": "K launches back to back between one HIP-event pair on the launch stream",
+                      "per_launch_event_us": round(us, 2),
+                      "per_launch_event_frac": round(alg / (us * 1e-6) / HBM_PEAK_BPS, 4)}}
+
+
 def config5_combine(m, lib, stream, k: int, w: int):
     """Config 5's combine at one GPU, in its element type (MPIX_C_FLOAT16,
     mpir_op_util.h:315-319; configure.ac:3122-3131):
@@ -1078,6 +1122,7 @@ def main():
         if nbytes >= 256 * MIB:
             out["config2_64MiB"] = config2(m, lib, pairs, s, args.steps, args.warmup)
             out["config5_combine"] = config5_combine(m, lib, s, args.steps, args.warmup)
+            out["config4_combine"] = config4_combine(m, s, args.steps, args.warmup)
 
         # ---- stream-ordered API, back to back (what the library's schedules drive)
         def sstep(i):

@@ -5,7 +5,7 @@
 //
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off \
 //         -Impich-pip_amd/csrc/hip -o tools/chain_shape tools/chain_shape.hip
-//   tools/chain_shape [rounds = 9]
+//   tools/chain_shape [rounds = 9] [chain | tree | p8]
 //
 // fp16 SUM CHAIN over p blocks of 1 GiB / p (config 5's sendbuf at p ranks),
 // two operand sets alternated, HIP events over batches of 10 back-to-back
@@ -43,53 +43,58 @@ struct Shape {
     int th, u, lds;
 };
 
-template <int P, int U, int TH>
+template <class T, int P, bool TREE, int U, int TH>
 void launch(const MultiArgs &a, int lds) {
     const uint64_t tile = (uint64_t)TH * U * 16;
-    hipLaunchKernelGGL((k_combine_multi<OpSum, f16, P, false, U, TH>), dim3((unsigned)(a.vbytes / tile)), dim3(TH),
+    hipLaunchKernelGGL((k_combine_multi<OpSum, T, P, TREE, U, TH>), dim3((unsigned)(a.vbytes / tile)), dim3(TH),
                        lds, 0, a);
 }
 
-template <int P>
-void run(int rounds) {
-    CK(hipFuncSetAttribute((const void *)k_combine_multi<OpSum, f16, P, false, 1, 1024>,
+// T / TREE / total: CHAIN fp16 over 1 GiB (config 5's sendbuf) by default;
+// TREE fp32 over `total` bytes for config 4's reduce-scatter blocks
+template <int P, class T = f16, bool TREE = false>
+void run(int rounds, uint64_t total = 1ull << 30) {
+    CK(hipFuncSetAttribute((const void *)k_combine_multi<OpSum, T, P, TREE, 1, 1024>,
                            hipFuncAttributeMaxDynamicSharedMemorySize, 96 << 10));
-    CK(hipFuncSetAttribute((const void *)k_combine_multi<OpSum, f16, P, false, 4, kThreads>,
+    CK(hipFuncSetAttribute((const void *)k_combine_multi<OpSum, T, P, TREE, 4, kThreads>,
                            hipFuncAttributeMaxDynamicSharedMemorySize, 96 << 10));
     const Shape shapes[] = {{"1024 x 1, 96 KiB cap (1 / CU)", 1024, 1, 96 << 10}, {"1024 x 1, no cap (2 / CU)", 1024, 1, 0},
                             {"256 x 4, 53 KiB cap (3 / CU)", 256, 4, 53 << 10}, {"256 x 4, 40 KiB cap (4 / CU)", 256, 4, 40 << 10},
                             {"256 x 4, no cap", 256, 4, 0}};
     constexpr int NS = 5;
-    const int lib = P >= 5 ? 0 : 2;     // (as launched before this probe)
-    const uint64_t block = ((1ull << 30) / P) / 65536 * 65536;       // bytes, a multiple of both tiles
-    std::vector<char *> bufs(2 * P + 2);
+    // the library: P = 8 over blocks of 128 MiB or more in 1024 x 1, everything else in 256 x 4
+    const int lib = (P >= 8 && (total / P) >= (128ull << 20)) ? 0 : 2;
+    const uint64_t block = (total / P) / 65536 * 65536;              // bytes, a multiple of both tiles
+    // operand sets rotated over at least 1.5 GiB (past the 256 MB Infinity Cache)
+    const int nsets = std::max<int>(2, (int)((3ull << 29) / ((P + 1) * block) + 1));
+    std::vector<char *> bufs(nsets * (P + 1));
     for (auto &b : bufs) CK(hipMalloc(&b, block));
-    for (int i = 0; i < 2 * P; ++i) k_fill<<<2048, 256>>>((uint16_t *)bufs[i], block / 2, 0x99u + 13u * i);
+    for (int i = 0; i < nsets * (P + 1); ++i) k_fill<<<2048, 256>>>((uint16_t *)bufs[i], block / 2, 0x99u + 13u * i);
     CK(hipDeviceSynchronize());
     auto args = [&](int set) {
         MultiArgs a{};
-        for (int j = 0; j < P; ++j) a.in[j] = bufs[set * P + j];
-        a.out = bufs[2 * P + set];
+        for (int j = 0; j < P; ++j) a.in[j] = bufs[set * (P + 1) + j];
+        a.out = bufs[set * (P + 1) + P];
         a.vbytes = block;
         a.keep = keep_for(block);
         return a;
     };
     auto go = [&](int si, int set) {
         const Shape &s = shapes[si];
-        if (s.th == 1024) launch<P, 1, 1024>(args(set), s.lds);
-        else launch<P, 4, kThreads>(args(set), s.lds);
+        if (s.th == 1024) launch<T, P, TREE, 1, 1024>(args(set), s.lds);
+        else launch<T, P, TREE, 4, kThreads>(args(set), s.lds);
     };
     std::vector<char> want(block), got(block);
     int bad = 0;
     go(lib, 0);
     CK(hipDeviceSynchronize());
-    CK(hipMemcpy(want.data(), bufs[2 * P], block, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(want.data(), bufs[P], block, hipMemcpyDeviceToHost));
     for (int si = 0; si < NS; ++si) {
         if (si == lib) continue;
-        CK(hipMemset(bufs[2 * P], 0, block));
+        CK(hipMemset(bufs[P], 0, block));
         go(si, 0);
         CK(hipDeviceSynchronize());
-        CK(hipMemcpy(got.data(), bufs[2 * P], block, hipMemcpyDeviceToHost));
+        CK(hipMemcpy(got.data(), bufs[P], block, hipMemcpyDeviceToHost));
         if (memcmp(got.data(), want.data(), block)) ++bad;
     }
     hipEvent_t e0, e1;
@@ -104,9 +109,9 @@ void run(int rounds) {
         for (int i = 0; i < NS; ++i) order[i] = i;
         std::shuffle(order, order + NS, rng);
         for (int si : order) {
-            go(si, k++ & 1);
+            go(si, k++ % nsets);
             CK(hipEventRecord(e0, 0));
-            for (int b = 0; b < batch; ++b) go(si, k++ & 1);
+            for (int b = 0; b < batch; ++b) go(si, k++ % nsets);
             CK(hipEventRecord(e1, 0));
             CK(hipEventSynchronize(e1));
             float ms = 0;
@@ -114,7 +119,8 @@ void run(int rounds) {
             if (r) us[si].push_back(ms * 1e3 / batch);
         }
     }
-    printf("CHAIN%d fp16, %d x %.1f MiB: outputs %s\n", P, P, block / 1048576.0, bad ? "DIFFER" : "identical");
+    printf("%s%d %s, %d x %.1f MiB, %d sets: outputs %s\n", TREE ? "TREE" : "CHAIN", P, sizeof(T) == 2 ? "fp16" : "fp32",
+           P, block / 1048576.0, nsets, bad ? "DIFFER" : "identical");
     for (int si = 0; si < NS; ++si) {
         std::sort(us[si].begin(), us[si].end());
         const double med = us[si][us[si].size() / 2];
@@ -128,10 +134,23 @@ void run(int rounds) {
 
 int main(int argc, char **argv) {
     const int rounds = argc > 1 ? atoi(argv[1]) : 9;
-    run<3>(rounds);
-    run<5>(rounds);
-    run<6>(rounds);
-    run<7>(rounds);
-    run<8>(rounds);     // config 5 at 8 ranks: the library's P = 8 shape against the others
+    const char *mode = argc > 2 ? argv[2] : "chain";
+    if (!strcmp(mode, "chain")) {
+        run<3>(rounds);
+        run<5>(rounds);
+        run<6>(rounds);
+        run<7>(rounds);
+        run<8>(rounds);     // config 5 at 8 ranks: the library's P = 8 shape against the others
+    } else if (!strcmp(mode, "tree")) {
+        // config 4's reduce-scatter folds: TREE8 fp32 over 8 x 32 MiB, TREE4 over 4 x 64 MiB
+        run<8, float, true>(rounds, 256ull << 20);
+        run<4, float, true>(rounds, 256ull << 20);
+    } else {
+        // P = 8 by block size: 32 / 64 / 128 MiB blocks, TREE fp32 and CHAIN fp16
+        for (uint64_t mib : {32, 64, 128}) {
+            run<8, float, true>(rounds, 8 * (mib << 20));
+            run<8, f16, false>(rounds, 8 * (mib << 20));
+        }
+    }
     return 0;
 }
