@@ -668,8 +668,8 @@ def config4_combine(m, stream, k: int, w: int):
     alg = 9 * blk * 4
     del sets, outs
     torch.cuda.empty_cache()
-    return {"tree8": {"blocks": 8, "block_MiB": 32, "kernel": "k_combine_multi<OpSum, float, P=8, TREE> "
-                      "(256 x 4 shape below 128 MiB blocks)", "kernel_us": round(us_b2b, 2),
+    return {"tree8": {"blocks": 8, "block_MiB": 32, "kernel": "k_combine_multi<OpSum, float, P=8, TREE>",
+                      "kernel_us": round(us_b2b, 2),
                       "frac": round(alg / (us_b2b * 1e-6) / HBM_PEAK_BPS, 4),
                       "timing": "K launches back to back between one HIP-event pair on the launch stream",
                       "per_launch_event_us": round(us, 2),

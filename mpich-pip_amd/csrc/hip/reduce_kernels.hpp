@@ -739,14 +739,17 @@ __global__ __launch_bounds__(kThreads) void k_combine_multi_elems(MultiArgs a, u
 #endif
 template <int P, int TH>
 constexpr int multi_cap_bytes() {
-    // P = 3-7, and P = 8 below kMultiWideBytes per operand, take P = 4's shape
-    // and cap: 256 x 4 at three per CU (tools/chain_shape.hip,
-    // profiles/r05/chain_shape*.log, p8_shape.log): CHAIN3-7 0.785-0.833 against
-    // 0.784-0.789 in the 1024 x 1 shape; P = 8 over 32 / 64 MiB blocks 0.779-0.799
-    // against 0.732-0.769, over 128 MiB 0.763-0.769 against 0.767-0.786
+    // P = 5-7 (CHAIN folds of non-power-of-two rank counts) take P = 8's shape
+    // and cap, P = 3 P = 4's: with the operands in one staging slab at
+    // stage_stride() apart, as the collectives lay them, 1024 x 1 at one per CU
+    // runs CHAIN5-7 0.765-0.773 against 0.749-0.762 for 256 x 4 at three per CU,
+    // and CHAIN3 0.779 against 0.816 (tools/chain_shape.hip chainslab,
+    // profiles/r05/chainslab_shape.log).  (With one allocation per operand the
+    // order reverses, also for P = 8 below 128 MiB: chain_shape.log,
+    // p8_shape*.log against slab_shape.log; the library follows its collectives.)
     return !MPIR_MULTI_CAP_LDS ? 0
-           : (P == 8 && TH == 1024) ? (96 << 10)
-           : (P >= 3 && TH == kThreads) ? (53 << 10) : 0;
+           : (P >= 5 && TH == 1024) ? (96 << 10)
+           : ((P == 4 || P == 3) && TH == kThreads) ? (53 << 10) : 0;
 }
 template <class Op, class T, int P, bool TREE, int U, int TH>
 size_t multi_lds_cap() {
@@ -870,28 +873,13 @@ hipError_t launch_combine_any(const void *const *ins, int n, int tree, void *out
     return hipGetLastError();
 }
 
-// P = 8 blocks of at least this many bytes run on 1024-thread workgroups, one
-// per CU; smaller ones (config 4's 8 x 32 MiB) on 256 x 4 at three per CU
-constexpr uint64_t kMultiWideBytes = 128ull << 20;
-
 template <class Op, class T, int P, bool TREE>
 hipError_t launch_combine_p(const void *const *ins, void *out_, uint64_t count, hipStream_t s) {
-    // (2, 4, 8 for TREE; every P of 2-8 for CHAIN).  Round 1-2 shapes: rocprofv3
-    // trace, 32 MiB blocks (profiles/archive/r01s3_multi_shape_p24.log): P = 4 with
-    // 4 vectors per lane 0.78-0.80 (2 vectors: 0.72-0.74); P = 2 with 4 vectors
-    // per lane 0.74-0.76.  Round 5 (multi_cap_bytes above): P = 3-8 in the same
-    // 256 x 4 shape under a three-per-CU cap, except P = 8 over blocks of
-    // kMultiWideBytes or more, which keeps 1024 x 1 at one per CU.
-    // (complex PROD keeps 1024 x 1 at every size: its Annex G recovery over 8 x 4
-    // vectors per lane needs scratch in the 256 x 4 shape)
-    constexpr bool cplx_prod = __is_same(Op, OpProd) && (__is_same(T, cf32) || __is_same(T, cf64));
-    if constexpr (P >= 8) {
-        if (cplx_prod || count * sizeof(T) >= kMultiWideBytes)
-            return launch_combine_pu<Op, T, P, TREE, 1, 1024>(ins, out_, count, s);
-    }
-    if constexpr (!(P >= 8 && cplx_prod))
-        return launch_combine_pu<Op, T, P, TREE, 4, kThreads>(ins, out_, count, s);
-    return hipSuccess;      // unreachable
+    // (2, 4, 8 for TREE; every P of 2-8 for CHAIN: 5-7 in P = 8's shape, 3 in
+    // P = 4's).  rocprofv3 trace, 32 MiB blocks (profiles/archive/r01s3_multi_shape_p24.log):
+    // P = 8 on 1024-thread WGs (0.76-0.80 of peak); P = 4 with 4 vectors per lane
+    // 0.78-0.80 (2 vectors: 0.72-0.74); P = 2 with 4 vectors per lane 0.74-0.76
+    return launch_combine_pu<Op, T, P, TREE, (P >= 5 ? 1 : 4), (P >= 5 ? 1024 : kThreads)>(ins, out_, count, s);
 }
 
 }  // namespace mpir_hip

@@ -5,7 +5,7 @@
 //
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off \
 //         -Impich-pip_amd/csrc/hip -o tools/chain_shape tools/chain_shape.hip
-//   tools/chain_shape [rounds = 9] [chain | tree | p8]
+//   tools/chain_shape [rounds = 9] [chain | chainslab | tree | p8 | slab]
 //
 // fp16 SUM CHAIN over p blocks of 1 GiB / p (config 5's sendbuf at p ranks),
 // two operand sets alternated, HIP events over batches of 10 back-to-back
@@ -53,7 +53,7 @@ void launch(const MultiArgs &a, int lds) {
 // T / TREE / total: CHAIN fp16 over 1 GiB (config 5's sendbuf) by default;
 // TREE fp32 over `total` bytes for config 4's reduce-scatter blocks
 template <int P, class T = f16, bool TREE = false>
-void run(int rounds, uint64_t total = 1ull << 30) {
+void run(int rounds, uint64_t total = 1ull << 30, uint64_t slab_skew = 0) {
     CK(hipFuncSetAttribute((const void *)k_combine_multi<OpSum, T, P, TREE, 1, 1024>,
                            hipFuncAttributeMaxDynamicSharedMemorySize, 96 << 10));
     CK(hipFuncSetAttribute((const void *)k_combine_multi<OpSum, T, P, TREE, 4, kThreads>,
@@ -66,9 +66,21 @@ void run(int rounds, uint64_t total = 1ull << 30) {
     const int lib = (P >= 8 && (total / P) >= (128ull << 20)) ? 0 : 2;
     const uint64_t block = (total / P) / 65536 * 65536;              // bytes, a multiple of both tiles
     // operand sets rotated over at least 1.5 GiB (past the 256 MB Infinity Cache)
+    // slab_skew != 0: each set is one allocation holding the P blocks at stride
+    // block + slab_skew and the output after them, as the collectives' staging
+    // slots (coll_hip.c stage_stride); else one allocation per block
     const int nsets = std::max<int>(2, (int)((3ull << 29) / ((P + 1) * block) + 1));
-    std::vector<char *> bufs(nsets * (P + 1));
-    for (auto &b : bufs) CK(hipMalloc(&b, block));
+    std::vector<char *> bufs(nsets * (P + 1)), slabs;
+    if (slab_skew) {
+        for (int set = 0; set < nsets; ++set) {
+            char *b;
+            CK(hipMalloc(&b, (P + 1) * (block + slab_skew)));
+            slabs.push_back(b);
+            for (int j = 0; j <= P; ++j) bufs[set * (P + 1) + j] = b + j * (block + slab_skew);
+        }
+    } else {
+        for (auto &b : bufs) CK(hipMalloc(&b, block));
+    }
     for (int i = 0; i < nsets * (P + 1); ++i) k_fill<<<2048, 256>>>((uint16_t *)bufs[i], block / 2, 0x99u + 13u * i);
     CK(hipDeviceSynchronize());
     auto args = [&](int set) {
@@ -119,8 +131,9 @@ void run(int rounds, uint64_t total = 1ull << 30) {
             if (r) us[si].push_back(ms * 1e3 / batch);
         }
     }
-    printf("%s%d %s, %d x %.1f MiB, %d sets: outputs %s\n", TREE ? "TREE" : "CHAIN", P, sizeof(T) == 2 ? "fp16" : "fp32",
-           P, block / 1048576.0, nsets, bad ? "DIFFER" : "identical");
+    printf("%s%d %s, %d x %.1f MiB, %d sets%s: outputs %s\n", TREE ? "TREE" : "CHAIN", P, sizeof(T) == 2 ? "fp16" : "fp32",
+           P, block / 1048576.0, nsets, slab_skew ? ", staging slab (stride block + 4352 B)" : ", one allocation per block",
+           bad ? "DIFFER" : "identical");
     for (int si = 0; si < NS; ++si) {
         std::sort(us[si].begin(), us[si].end());
         const double med = us[si][us[si].size() / 2];
@@ -129,13 +142,20 @@ void run(int rounds, uint64_t total = 1ull << 30) {
     }
     CK(hipEventDestroy(e0));
     CK(hipEventDestroy(e1));
-    for (auto b : bufs) CK(hipFree(b));
+    if (slab_skew) for (auto b : slabs) CK(hipFree(b));
+    else for (auto b : bufs) CK(hipFree(b));
 }
 
 int main(int argc, char **argv) {
     const int rounds = argc > 1 ? atoi(argv[1]) : 9;
     const char *mode = argc > 2 ? argv[2] : "chain";
-    if (!strcmp(mode, "chain")) {
+    if (!strcmp(mode, "chainslab")) {
+        // the pairwise chain's operands as the collective lays them: one staging slab
+        run<3>(rounds, 1ull << 30, 4352);
+        run<5>(rounds, 1ull << 30, 4352);
+        run<6>(rounds, 1ull << 30, 4352);
+        run<7>(rounds, 1ull << 30, 4352);
+    } else if (!strcmp(mode, "chain")) {
         run<3>(rounds);
         run<5>(rounds);
         run<6>(rounds);
@@ -146,10 +166,12 @@ int main(int argc, char **argv) {
         run<8, float, true>(rounds, 256ull << 20);
         run<4, float, true>(rounds, 256ull << 20);
     } else {
-        // P = 8 by block size: 32 / 64 / 128 MiB blocks, TREE fp32 and CHAIN fp16
+        // P = 8 by block size: 32 / 64 / 128 MiB blocks, TREE fp32 and CHAIN fp16;
+        // mode "slab": the blocks in one allocation at the staging stride
+        const uint64_t skew = !strcmp(mode, "slab") ? 4352 : 0;
         for (uint64_t mib : {32, 64, 128}) {
-            run<8, float, true>(rounds, 8 * (mib << 20));
-            run<8, f16, false>(rounds, 8 * (mib << 20));
+            run<8, float, true>(rounds, 8 * (mib << 20), skew);
+            run<8, f16, false>(rounds, 8 * (mib << 20), skew);
         }
     }
     return 0;
