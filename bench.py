@@ -687,7 +687,7 @@ def config5_combine(m, lib, stream, k: int, w: int):
                    (reduce_scatter_block_intra_pairwise.c:97-134): 8 blocks of
                    128 MiB, ((x0+x1)+x2)+...+x7 into a 128 MiB output, the blocks
                    at the collective's skewed staging stride (coll_hip.c
-                   stage_stride: 128 MiB + 4352 B), two sets alternated (2.25 GiB a
+                   stage_stride: 128 MiB + 6400 B), two sets alternated (2.25 GiB a
                    cycle, past the 256 MB Infinity Cache); HIP events on the stream.
     Fractions are algorithmic bytes (3 x 256 MiB; 9 x 128 MiB) over kernel time
     against 8.0 TB/s; per-launch HBM traffic from the committed PMC summary."""
@@ -715,7 +715,7 @@ def config5_combine(m, lib, stream, k: int, w: int):
     torch.cuda.empty_cache()
 
     blk = 64 * MIB                              # halves in 128 MiB
-    stride = (blk * 2 + 4352) // 2              # coll_hip.c stage_stride, in halves
+    stride = (blk * 2 + 6400) // 2              # coll_hip.c stage_stride (128 MiB blocks: + 6400 B), in halves
     sets = [torch.empty(8 * stride, device="cuda", dtype=torch.float16) for _ in range(2)]
     outs = [torch.empty(blk, device="cuda", dtype=torch.float16) for _ in range(2)]
     for s_ in sets:

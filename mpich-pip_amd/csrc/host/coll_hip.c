@@ -349,11 +349,18 @@ static int group_exchange(struct MPIX_Hip_comm_s *c, const xfer_t *sends, int ns
  * combine on the same HBM channels at the same moment: 8 x 32 MiB TREE8 fp32
  * ran at 0.689 of the HBM peak with a 32 MiB stride, 0.767 with 32 MiB +
  * 4352 B (4 KiB + 256), 0.717 with + 256 B only (rocprofv3 kernel trace,
- * tools/multi_gap_ab.hip, profiles/archive/r01s3_multi_skew_ab.log).  The skew keeps
- * the 256 B alignment (fused kernels need the operands equal mod 16). */
+ * tools/multi_gap_ab.hip, profiles/archive/r01s3_multi_skew_ab.log).  The best
+ * skew depends on the block size (the address bits the blocks themselves set):
+ * around 128 MiB blocks (config 5's 8 x 128 MiB CHAIN8) 6400 B ran 1.3-4.5
+ * points above 4352 B in seven sweeps on five boxes, at 32 / 64 MiB 0.3-1 point
+ * below it, at 256 MiB within a point (tools/fold_skew.hip, chain_shape.hip
+ * slabskew; profiles/r05/fold_skew*.log, slabskew.log).  The skew keeps the
+ * 256 B alignment (fused kernels need the operands equal mod 16). */
 static size_t stage_stride(size_t bytes)
 {
     size_t st = (bytes + 255) & ~(size_t) 255;
+    if (st >= ((size_t) 96 << 20) && st < ((size_t) 192 << 20))
+        return st + 6400;
     return st >= ((size_t) 1 << 20) ? st + 4352 : st;
 }
 

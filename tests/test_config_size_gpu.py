@@ -53,9 +53,10 @@ def test_config2_64mib_vs_oracle(mpi, orc, cuda, extra, off):
 
 def _staged(torch, blocks):
     """The blocks at coll_hip.c's staging stride (slot rounded to 256 B, + 4352 B
-    from 1 MiB up), as the all-to-all leaves them."""
+    from 1 MiB up, + 6400 B for slots of 96-192 MiB), as the all-to-all leaves them."""
     nb = blocks[0].nbytes
-    stride = ((nb + 255) & ~255) + (4352 if nb >= MIB else 0)
+    st = (nb + 255) & ~255
+    stride = st + (6400 if 96 * MIB <= st < 192 * MIB else (4352 if st >= MIB else 0))
     buf = torch.zeros(stride * len(blocks), dtype=torch.uint8, device="cuda")
     for j, blk in enumerate(blocks):
         buf[j * stride:j * stride + nb] = torch.from_numpy(blk.view(np.uint8))

@@ -5,7 +5,7 @@
 //
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off \
 //         -Impich-pip_amd/csrc/hip -o tools/chain_shape tools/chain_shape.hip
-//   tools/chain_shape [rounds = 9] [chain | chainslab | tree | p8 | slab]
+//   tools/chain_shape [rounds = 9] [chain | chainslab | tree | p8 | slab | slabskew]
 //
 // fp16 SUM CHAIN over p blocks of 1 GiB / p (config 5's sendbuf at p ranks),
 // two operand sets alternated, HIP events over batches of 10 back-to-back
@@ -132,7 +132,7 @@ void run(int rounds, uint64_t total = 1ull << 30, uint64_t slab_skew = 0) {
         }
     }
     printf("%s%d %s, %d x %.1f MiB, %d sets%s: outputs %s\n", TREE ? "TREE" : "CHAIN", P, sizeof(T) == 2 ? "fp16" : "fp32",
-           P, block / 1048576.0, nsets, slab_skew ? ", staging slab (stride block + 4352 B)" : ", one allocation per block",
+           P, block / 1048576.0, nsets, slab_skew ? ", staging slab" : ", one allocation per block",
            bad ? "DIFFER" : "identical");
     for (int si = 0; si < NS; ++si) {
         std::sort(us[si].begin(), us[si].end());
@@ -149,7 +149,14 @@ void run(int rounds, uint64_t total = 1ull << 30, uint64_t slab_skew = 0) {
 int main(int argc, char **argv) {
     const int rounds = argc > 1 ? atoi(argv[1]) : 9;
     const char *mode = argc > 2 ? argv[2] : "chain";
-    if (!strcmp(mode, "chainslab")) {
+    if (!strcmp(mode, "slabskew")) {
+        // config 4 / 5's P = 8 folds in the staging slab at several skews
+        for (uint64_t skew : {4352ull, 6400ull, 2097152ull, 2097408ull}) {
+            printf("== slab skew %llu B\n", (unsigned long long)skew);
+            run<8, float, true>(rounds, 256ull << 20, skew);
+            run<8, f16, false>(rounds, 1ull << 30, skew);
+        }
+    } else if (!strcmp(mode, "chainslab")) {
         // the pairwise chain's operands as the collective lays them: one staging slab
         run<3>(rounds, 1ull << 30, 4352);
         run<5>(rounds, 1ull << 30, 4352);
