@@ -5,7 +5,7 @@
 //
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off \
 //         -Impich-pip_amd/csrc/hip -o tools/chain_shape tools/chain_shape.hip
-//   tools/chain_shape [rounds = 9] [chain | chainslab | tree | p8 | slab | slabskew]
+//   tools/chain_shape [rounds = 9] [chain | chainslab | chainskew | tree | p8 | slab | slabskew]
 //
 // fp16 SUM CHAIN over p blocks of 1 GiB / p (config 5's sendbuf at p ranks),
 // two operand sets alternated, HIP events over batches of 10 back-to-back
@@ -62,8 +62,8 @@ void run(int rounds, uint64_t total = 1ull << 30, uint64_t slab_skew = 0) {
                             {"256 x 4, 53 KiB cap (3 / CU)", 256, 4, 53 << 10}, {"256 x 4, 40 KiB cap (4 / CU)", 256, 4, 40 << 10},
                             {"256 x 4, no cap", 256, 4, 0}};
     constexpr int NS = 5;
-    // the library: P = 8 over blocks of 128 MiB or more in 1024 x 1, everything else in 256 x 4
-    const int lib = (P >= 8 && (total / P) >= (128ull << 20)) ? 0 : 2;
+    // the library: P = 5-8 in 1024 x 1, P = 2-4 in 256 x 4
+    const int lib = P >= 5 ? 0 : 2;
     const uint64_t block = (total / P) / 65536 * 65536;              // bytes, a multiple of both tiles
     // operand sets rotated over at least 1.5 GiB (past the 256 MB Infinity Cache)
     // slab_skew != 0: each set is one allocation holding the P blocks at stride
@@ -149,7 +149,14 @@ void run(int rounds, uint64_t total = 1ull << 30, uint64_t slab_skew = 0) {
 int main(int argc, char **argv) {
     const int rounds = argc > 1 ? atoi(argv[1]) : 9;
     const char *mode = argc > 2 ? argv[2] : "chain";
-    if (!strcmp(mode, "slabskew")) {
+    if (!strcmp(mode, "chainskew")) {
+        // the pairwise chain at 6 and 7 ranks (171 / 146 MiB slots) at both skews
+        for (uint64_t skew : {4352ull, 6400ull}) {
+            printf("== slab skew %llu B\n", (unsigned long long)skew);
+            run<6>(rounds, 1ull << 30, skew);
+            run<7>(rounds, 1ull << 30, skew);
+        }
+    } else if (!strcmp(mode, "slabskew")) {
         // config 4 / 5's P = 8 folds in the staging slab at several skews
         for (uint64_t skew : {4352ull, 6400ull, 2097152ull, 2097408ull}) {
             printf("== slab skew %llu B\n", (unsigned long long)skew);
