@@ -5,7 +5,7 @@
 //
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off \
 //         -Impich-pip_amd/csrc/hip -o tools/chain_shape tools/chain_shape.hip
-//   tools/chain_shape [rounds = 9] [chain | chainslab | chainskew | tree | p8 | slab | slabskew]
+//   tools/chain_shape [rounds = 9] [chain | chainslab | chainskew | p4slab | tree | p8 | slab | slabskew]
 //
 // fp16 SUM CHAIN over p blocks of 1 GiB / p (config 5's sendbuf at p ranks),
 // two operand sets alternated, HIP events over batches of 10 back-to-back
@@ -149,7 +149,11 @@ void run(int rounds, uint64_t total = 1ull << 30, uint64_t slab_skew = 0) {
 int main(int argc, char **argv) {
     const int rounds = argc > 1 ? atoi(argv[1]) : 9;
     const char *mode = argc > 2 ? argv[2] : "chain";
-    if (!strcmp(mode, "chainskew")) {
+    if (!strcmp(mode, "p4slab")) {
+        // config 4 / 5 at 4 ranks in the staging slab: TREE4 fp32 4 x 64 MiB, CHAIN4 fp16 4 x 256 MiB
+        run<4, float, true>(rounds, 256ull << 20, 4352);
+        run<4, f16, false>(rounds, 1ull << 30, 4352);
+    } else if (!strcmp(mode, "chainskew")) {
         // the pairwise chain at 6 and 7 ranks (171 / 146 MiB slots) at both skews
         for (uint64_t skew : {4352ull, 6400ull}) {
             printf("== slab skew %llu B\n", (unsigned long long)skew);
