@@ -5,7 +5,7 @@
 //
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off \
 //         -Impich-pip_amd/csrc/hip -o tools/chain_shape tools/chain_shape.hip
-//   tools/chain_shape [rounds = 9] [chain | chainslab | chainskew | p4slab | tree | p8 | slab | slabskew]
+//   tools/chain_shape [rounds = 9] [chain | chainslab | chainskew | p2slab | p4slab | tree | p8 | slab | slabskew]
 //
 // fp16 SUM CHAIN over p blocks of 1 GiB / p (config 5's sendbuf at p ranks),
 // two operand sets alternated, HIP events over batches of 10 back-to-back
@@ -62,8 +62,8 @@ void run(int rounds, uint64_t total = 1ull << 30, uint64_t slab_skew = 0) {
                             {"256 x 4, 53 KiB cap (3 / CU)", 256, 4, 53 << 10}, {"256 x 4, 40 KiB cap (4 / CU)", 256, 4, 40 << 10},
                             {"256 x 4, no cap", 256, 4, 0}};
     constexpr int NS = 5;
-    // the library: P = 5-8 in 1024 x 1, P = 2-4 in 256 x 4
-    const int lib = P >= 5 ? 0 : 2;
+    // the library: P = 5-8 in 1024 x 1, P = 3-4 in 256 x 4 capped, P = 2 uncapped
+    const int lib = P >= 5 ? 0 : (P == 2 ? 4 : 2);
     const uint64_t block = (total / P) / 65536 * 65536;              // bytes, a multiple of both tiles
     // operand sets rotated over at least 1.5 GiB (past the 256 MB Infinity Cache)
     // slab_skew != 0: each set is one allocation holding the P blocks at stride
@@ -149,7 +149,11 @@ void run(int rounds, uint64_t total = 1ull << 30, uint64_t slab_skew = 0) {
 int main(int argc, char **argv) {
     const int rounds = argc > 1 ? atoi(argv[1]) : 9;
     const char *mode = argc > 2 ? argv[2] : "chain";
-    if (!strcmp(mode, "p4slab")) {
+    if (!strcmp(mode, "p2slab")) {
+        // config 4 / 5 at 2 ranks in the staging slab: TREE2 fp32 2 x 128 MiB, CHAIN2 fp16 2 x 512 MiB
+        run<2, float, true>(rounds, 256ull << 20, 6400);
+        run<2, f16, false>(rounds, 1ull << 30, 4352);
+    } else if (!strcmp(mode, "p4slab")) {
         // config 4 / 5 at 4 ranks in the staging slab: TREE4 fp32 4 x 64 MiB, CHAIN4 fp16 4 x 256 MiB
         run<4, float, true>(rounds, 256ull << 20, 4352);
         run<4, f16, false>(rounds, 1ull << 30, 4352);
