@@ -879,6 +879,14 @@ hipError_t launch_combine_p(const void *const *ins, void *out_, uint64_t count, 
     // P = 4's).  rocprofv3 trace, 32 MiB blocks (profiles/archive/r01s3_multi_shape_p24.log):
     // P = 8 on 1024-thread WGs (0.76-0.80 of peak); P = 4 with 4 vectors per lane
     // 0.78-0.80 (2 vectors: 0.72-0.74); P = 2 with 4 vectors per lane 0.74-0.76
+    // P = 2 over blocks of 256 MiB or more (config 5's 2 x 512 MiB at 2 ranks) on
+    // 1024 x 1, uncapped: 0.798-0.808 against 0.784-0.788 for 256 x 4 in the
+    // staging slab; over 128 MiB the two tie (tools/chain_shape.hip p2slab,
+    // profiles/r05/p2slab*.log)
+    if constexpr (P == 2) {
+        if (count * sizeof(T) >= (256ull << 20))
+            return launch_combine_pu<Op, T, 2, TREE, 1, 1024>(ins, out_, count, s);
+    }
     return launch_combine_pu<Op, T, P, TREE, (P >= 5 ? 1 : 4), (P >= 5 ? 1024 : kThreads)>(ins, out_, count, s);
 }
 

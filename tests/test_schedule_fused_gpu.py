@@ -327,3 +327,34 @@ def test_fused_full_size_blocks(mpi, orc, cuda, t, order, block_mib):
             assert orc.reduce_local(acc[j], acc[0], n, dt, o, check=False) == 0
     got = out.cpu().numpy().view(np.uint8)
     assert np.array_equal(got, acc[0]), f"{np.count_nonzero(got != acc[0])} bytes differ"
+
+
+@pytest.mark.parametrize("t,order,nbytes", [("MPI_FLOAT", "TREE", (256 << 20) + 20), ("MPIX_C_FLOAT16", "CHAIN", (512 << 20) + 6)],
+                         ids=["tree2-fp32-256MiB", "chain2-fp16-512MiB"])
+def test_two_operand_fold_large_blocks(mpi, orc, cuda, t, order, nbytes):
+    """Two-operand folds over blocks of 256 MiB and more run on the 1024 x 1
+    shape (launch_combine_p; config 5's 2 x 512 MiB at 2 ranks), with the
+    operands one element past 16 B alignment so the head and tail run too;
+    bit-exact against the oracle's MPIR_Reduce_local step."""
+    torch = cuda
+    esz = T.elem_size(t)
+    n = nbytes // esz
+    dt, o = mpi.DATATYPES[t], mpi.OPS["MPI_SUM"]
+    g = torch.Generator(device="cuda").manual_seed(n)
+    if t == "MPI_FLOAT":
+        dev = [torch.rand(n + 1, device="cuda", generator=g) * 2 - 1 for _ in range(2)]
+    else:
+        dev = [(torch.rand(n + 1, device="cuda", generator=g) * 8 - 4).half() for _ in range(2)]
+    out = torch.zeros_like(dev[0])
+    torch.cuda.synchronize()
+    ptrs = [d.data_ptr() + esz for d in dev]
+    rc = mpi.reduce_local_multi(ptrs, out.data_ptr() + esz, n, dt, o,
+                                mpi.MPIX_ORDER_TREE if order == "TREE" else mpi.MPIX_ORDER_CHAIN)
+    assert rc == 0, mpi.error_string(rc)
+    torch.cuda.synchronize()
+    acc = [d.cpu().numpy().view(np.uint8)[esz:].copy() for d in dev]
+    del dev
+    assert orc.reduce_local(acc[1], acc[0], n, dt, o, check=False) == 0
+    got = out.cpu().numpy().view(np.uint8)
+    assert not got[:esz].any(), "wrote before the output"
+    assert np.array_equal(got[esz:], acc[0]), f"{np.count_nonzero(got[esz:] != acc[0])} bytes differ"

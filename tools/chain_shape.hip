@@ -153,6 +153,9 @@ int main(int argc, char **argv) {
         // config 4 / 5 at 2 ranks in the staging slab: TREE2 fp32 2 x 128 MiB, CHAIN2 fp16 2 x 512 MiB
         run<2, float, true>(rounds, 256ull << 20, 6400);
         run<2, f16, false>(rounds, 1ull << 30, 4352);
+        // the other sizes of the same two shapes
+        run<2, float, true>(rounds, 1ull << 30, 4352);
+        run<2, f16, false>(rounds, 256ull << 20, 6400);
     } else if (!strcmp(mode, "p4slab")) {
         // config 4 / 5 at 4 ranks in the staging slab: TREE4 fp32 4 x 64 MiB, CHAIN4 fp16 4 x 256 MiB
         run<4, float, true>(rounds, 256ull << 20, 4352);
