@@ -1,4 +1,4 @@
-"""The committed bench line (profiles/r05/bench_r05am.log, measured on MI355X) against
+"""The committed bench line (profiles/r05/bench_r05au.log, measured on MI355X) against
 the driver's contract and against itself: BASELINE.json's metric, the
 required keys, value = algorithmic bytes x N / time, roofline.frac =
 achieved / peak with achieved = 805,306,368 B / mean launch time, and the
@@ -10,7 +10,7 @@ import os
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LINE = os.path.join(ROOT, "profiles", "r05", "bench_r05am.log")
+LINE = os.path.join(ROOT, "profiles", "r05", "bench_r05au.log")
 GIB = float(1 << 30)
 
 
