@@ -412,14 +412,15 @@ def process_env(name: str) -> str:
 
 def variant_child(args) -> None:
     """--variant-child: the headline loop and its fresh-argument twin in this
-    process's environment (the parent sets HSA_ALLOCATE_QUEUE_DEV_MEM=0);
-    one JSON line."""
+    process's environment (the parent sets HSA_ALLOCATE_QUEUE_DEV_MEM=0, or
+    BENCH_BIND=none); one JSON line."""
     import torch
     import mpich_pip_amd as m
     lib = m.load()
     lib.MPIX_Reduce_local_set_errhandler(m.MPI_ERRORS_RETURN)
     reduce_local = m.fast_reduce_local()
     torch.cuda.set_device(0)
+    bind = bind_near_gpu(m, 0)
     count = args.mib * MIB // 4
     g = torch.Generator(device="cuda").manual_seed(0x5EED)
     pairs = [((torch.rand(count + SLACK // 4, device="cuda", generator=g) * 2 - 1),
@@ -429,16 +430,19 @@ def variant_child(args) -> None:
     dt, dtf, writes, _, _ = sync_loops(m, lib, reduce_local, ptrs, count, args.steps, args.warmup,
                                        torch.cuda.synchronize, lambda: None, lambda x: x,
                                        c_loop=m.fast_reduce_local_loop())
+    place = placement_record(m, 0)
     print(json.dumps({"dt": dt, "dt_fresh": dtf, "kernarg_writes_per_fresh_call": writes,
                       "HSA_ALLOCATE_QUEUE_DEV_MEM": process_env("HSA_ALLOCATE_QUEUE_DEV_MEM"),
-                      "direct_state": lib.MPIR_Hip_direct_state(0)}), flush=True)
+                      "direct_state": lib.MPIR_Hip_direct_state(0), "bind": bind,
+                      "placement": {k: place[k] for k in ("cpu", "cpu_node", "gpu_node")}}), flush=True)
 
 
-def run_variant_child(args) -> dict:
+def run_variant_child(args, env_over: dict | None = None) -> dict:
     """Start --variant-child with ROCm's own AQL ring placement
-    (HSA_ALLOCATE_QUEUE_DEV_MEM=0); called before this process touches a GPU."""
+    (HSA_ALLOCATE_QUEUE_DEV_MEM=0), or with `env_over`; called before this
+    process touches a GPU."""
     import subprocess
-    env = dict(os.environ, HSA_ALLOCATE_QUEUE_DEV_MEM="0")
+    env = dict(os.environ, **(env_over or {"HSA_ALLOCATE_QUEUE_DEV_MEM": "0"}))
     cmd = [sys.executable, os.path.abspath(__file__), "--variant-child", "--steps", str(args.steps),
            "--warmup", str(args.warmup), "--mib", str(args.mib)]
     try:
@@ -468,12 +472,16 @@ def event_launch_us(launch, k: int, w: int, stream, stat: str = "mean") -> float
     return sum(ms) / k * 1e3
 
 
-def direct_kernel_ns(lib, call, k: int, w: int):
+def direct_kernel_ns(lib, call, k: int, w: int, splits: list | None = None):
     """Device durations (ns) of the kernels K synchronous calls run through the
     direct AQL dispatch: the CP's dispatch start / end timestamps
     (MPIR_Hip_direct_profile; what rocprofv3 reports), or None where the
-    direct path did not take the calls (then the caller uses HIP events)."""
+    direct path did not take the calls (then the caller uses HIP events).
+    `splits`, if given, receives each call's timeline (MPIR_Hip_direct_last_split:
+    ns from entering the dispatch to the doorbell, the CP's start and end, and
+    the host seeing the completion signal)."""
     lib.MPIR_Hip_direct_profile(1)
+    sp = (ctypes.c_uint64 * 4)()
     try:
         for i in range(w):
             call(i)
@@ -482,11 +490,115 @@ def direct_kernel_ns(lib, call, k: int, w: int):
         for i in range(k):
             call(w + i)
             ns.append(lib.MPIR_Hip_direct_last_kernel_ns())
+            if splits is not None:
+                lib.MPIR_Hip_direct_last_split(sp)
+                splits.append(tuple(sp))
         if lib.MPIR_Hip_direct_dispatches() - before != k or min(ns) <= 0:
             return None
         return ns
     finally:
         lib.MPIR_Hip_direct_profile(0)
+
+
+def split_medians(splits: list) -> dict | None:
+    """Medians (us) of the synchronous call's intervals over the profiled calls'
+    timelines (direct_kernel_ns): entry -> doorbell (host), doorbell -> CP
+    dispatch start, the kernel (CP start -> end), CP end -> host sees the
+    completion signal.  The profiled calls run on the timestamped twin queue."""
+    rows = [s for s in splits if 0 < s[0] <= s[1] <= s[2] <= s[3]]
+    if not rows:
+        return None
+
+    def med(v):
+        v = sorted(v)
+        return round(v[len(v) // 2] * 1e-3, 2)
+    return {"calls": len(rows),
+            "host_to_doorbell_us": med([s[0] for s in rows]),
+            "doorbell_to_dispatch_start_us": med([s[1] - s[0] for s in rows]),
+            "kernel_us": med([s[2] - s[1] for s in rows]),
+            "end_to_host_seen_us": med([s[3] - s[2] for s in rows]),
+            "source": "MPIR_Hip_direct_last_split over the K profiled calls (timestamped twin queue; host clock "
+                      "stamps around the CP's dispatch timestamps)"}
+
+
+def placement_record(m, dev: int) -> dict:
+    """Where this rank's calling thread runs relative to its GPU
+    (MPIR_Hip_direct_placement), and the CPUs it may run on."""
+    rec = m.placement(dev)
+    try:
+        allowed = sorted(os.sched_getaffinity(0))
+    except OSError:
+        allowed = []
+    nodes = sorted({cpu_node(c) for c in allowed})
+    rec["allowed_cpus"] = len(allowed)
+    rec["allowed_nodes"] = nodes
+    return rec
+
+
+def node_cpus(node: int) -> set:
+    """CPUs of NUMA node `node` (sysfs cpulist)."""
+    out = set()
+    try:
+        txt = open(f"/sys/devices/system/node/node{node}/cpulist").read().strip()
+    except OSError:
+        return out
+    for part in txt.split(","):
+        if "-" in part:
+            a, b = part.split("-")
+            out.update(range(int(a), int(b) + 1))
+        elif part:
+            out.add(int(part))
+    return out
+
+
+def bind_near_gpu(m, dev: int) -> dict:
+    """Bind the calling thread (the one that makes the timed calls) to the CPUs
+    of its GPU's NUMA node, within the CPUs the job may use -- what a launcher's
+    binding does for a GPU rank (Hydra -bind-to, Slurm --cpu-bind / numactl
+    --cpunodebind).  Near against far callers, alternated fresh processes on one
+    box (tools/placement_ab.py, DESIGN.md §(d) "Where the caller runs"): the
+    synchronous call ~2 us faster near.  BENCH_BIND=none keeps the placement the
+    process was launched with."""
+    if os.environ.get("BENCH_BIND", "gpu-node") == "none":
+        return {"mode": "none (as launched)"}
+    gnode = m.placement(dev)["gpu_node"]
+    try:
+        allowed = os.sched_getaffinity(0)
+    except OSError:
+        return {"mode": "unbound", "reason": "no affinity interface"}
+    want = node_cpus(gnode) & allowed if gnode >= 0 else set()
+    if not want:
+        return {"mode": "unbound", "reason": f"no allowed CPU on the GPU's node ({gnode})", "gpu_node": gnode}
+    os.sched_setaffinity(0, want)          # this thread (and the threads it starts later)
+    return {"mode": "gpu-node", "gpu_node": gnode, "cpus": len(want), "of_allowed": len(allowed)}
+
+
+def library_hip_runtime(lib):
+    """The HIP runtime libmpir_hip.so links (as loaded in this process, found
+    through dladdr of one of its symbols), or None if it cannot be opened."""
+    try:
+        class DlInfo(ctypes.Structure):
+            _fields_ = [("dli_fname", ctypes.c_char_p), ("dli_fbase", ctypes.c_void_p),
+                        ("dli_sname", ctypes.c_char_p), ("dli_saddr", ctypes.c_void_p)]
+        libdl = ctypes.CDLL(None)
+        info = DlInfo()
+        # hipHostRegister as libmpich_reduce_local.so resolved it
+        addr = ctypes.cast(ctypes.CDLL(lib._name).hipHostRegister, ctypes.c_void_p).value
+        if addr and libdl.dladdr(ctypes.c_void_p(addr), ctypes.byref(info)) and info.dli_fname:
+            return ctypes.CDLL(info.dli_fname.decode())
+        return ctypes.CDLL("libamdhip64.so.7")
+    except (OSError, AttributeError):
+        return None
+
+
+def cpu_node(cpu: int) -> int:
+    try:
+        for e in os.listdir(f"/sys/devices/system/cpu/cpu{cpu}"):
+            if e.startswith("node") and e[4:].isdigit():
+                return int(e[4:])
+    except OSError:
+        pass
+    return -1
 
 
 def config3_sweep(m, lib, pairs, nbytes: int, stream, k: int = 15, w: int = 5):
@@ -852,9 +964,11 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # ROCm's own ring placement, in a child, before this process starts the GPU
-    ring_variant = None
+    ring_variant = launch_variant = None
     if world == 1 and not args.no_extras and not args.no_variants:
         ring_variant = run_variant_child(args)
+        # the headline loop with the process left where it was launched
+        launch_variant = run_variant_child(args, {"BENCH_BIND": "none"})
     # configs 4-5 (RCCL collectives) in a child per rank, also before this
     # process starts the GPU: one process per rank holds a GPU at any time
     # (a child beside a live rank would double the processes on each card)
@@ -881,6 +995,9 @@ def main():
     share = os.environ.get("BENCH_TEST_SHARE_GPU") == "1"
     dev = local % torch.cuda.device_count() if share else local
     torch.cuda.set_device(dev)
+    # the rank's calling thread near its GPU, as a launcher binds GPU ranks
+    # (value_conditions.placement; BENCH_BIND=none keeps the launch placement)
+    bind = bind_near_gpu(m, dev)
     if args.only_config5:
         print(json.dumps({"config5_combine": config5_combine(m, lib, torch.cuda.Stream(), args.steps, args.warmup)}),
               flush=True)
@@ -953,6 +1070,7 @@ def main():
     except ImportError:     # extension not built: the same C entry point through ctypes
         reduce_local, c_loop, binding = lib.MPI_Reduce_local, None, "ctypes"
     own, calls, gap = [], [], []
+    place_before = m.placement(dev)
     d_before = lib.MPIR_Hip_direct_dispatches()
     dt, dt_fresh, fresh_writes, step, dt_py = sync_loops(m, lib, reduce_local, ptrs, count, args.steps,
                                                          args.warmup, sync, barrier, max_over_ranks, own, c_loop,
@@ -970,9 +1088,13 @@ def main():
     value = alg_bytes * args.steps * world / dt / GIB
     # each rank's own figures beside the max-over-ranks `value`: a lagging GPU,
     # or a rank whose calls left the direct path, shows here
+    # where the timed loop's thread ran, relative to the GPU
+    place = placement_record(m, dev)
     rows = gather_rows([float(rank), float(dev), own[0], own[1], float(lib.MPIR_Hip_direct_state(dev)),
                         direct_share, cstats["median_us"], cstats["p10_us"], cstats["p90_us"],
-                        cstats["slow_share"]], world, dist,
+                        cstats["slow_share"], float(place_before["cpu"]), float(place["cpu"]),
+                        float(place["cpu_node"]), float(place["gpu_node"]), float(place["signal_node"]),
+                        float(place["error_word_node"]), float(place["allowed_cpus"])], world, dist,
                        "cpu" if pg_backend == "gloo" else "cuda")
 
     def rate(seconds):
@@ -1003,6 +1125,8 @@ def main():
             "runtime": {"HSA_ALLOCATE_QUEUE_DEV_MEM": process_env("HSA_ALLOCATE_QUEUE_DEV_MEM"),
                         "HSA_ALLOCATE_QUEUE_DEV_MEM_in_job_environment": os.environ.get("HSA_ALLOCATE_QUEUE_DEV_MEM")},
             "process_group": pg_backend,
+            # which sources the loaded binaries were built from (Makefile BUILD_ID)
+            "build_id": m.build_id(),
         },
         "value_conditions": {
             "headline": "value",
@@ -1012,6 +1136,10 @@ def main():
                                 "cache hit); sync_variants.fresh_args misses on every call" % (NPAIRS, NPAIRS),
             "caller": "K synchronous MPI_Reduce_local calls back to back from C (" + binding + "); "
                       "sync_variants.python_loop steps the same calls from Python",
+            "placement": dict(bind, note="the timed calls' thread bound to the CPUs of its GPU's NUMA node "
+                              "within the job's cpuset, as a launcher's -bind-to / --cpu-bind=closest would; "
+                              "sync_variants.launch_placement: the same loop left where the process was launched "
+                              "(BENCH_BIND=none)"),
             "warmup": "W untimed steps, the last of them after the barrier (BENCH_WARMUP_ORDER="
                       + os.environ.get("BENCH_WARMUP_ORDER", "late") + "), then a device sync and the K timed "
                       "steps: the first timed call does not pay the command processor's idle wake-up "
@@ -1028,7 +1156,10 @@ def main():
                       "frac_of_hbm_peak": round(alg_bytes * args.steps / r[2] / HBM_PEAK_BPS, 4),
                       "fresh_args_seconds": round(r[3], 6), "direct_state": int(r[4]),
                       "direct_share": round(r[5], 4),
-                      "call_median_us": r[6], "call_p10_p90_us": [r[7], r[8]], "slow_share": r[9]}
+                      "call_median_us": r[6], "call_p10_p90_us": [r[7], r[8]], "slow_share": r[9],
+                      "placement": {"cpu_before_loop": int(r[10]), "cpu_after_loop": int(r[11]),
+                                    "cpu_node": int(r[12]), "gpu_node": int(r[13]), "signal_node": int(r[14]),
+                                    "error_word_node": int(r[15]), "allowed_cpus": int(r[16])}}
                      for r in rows],
         # rank 0's K timed calls, each on its own (clock stamps in the C loop)
         "call_distribution": dict(cstats, source="CLOCK_MONOTONIC after each call of the timed C loop (rank 0)"
@@ -1050,6 +1181,14 @@ def main():
                 "direct_state": ring_variant.get("direct_state")}
         else:
             variants["rocm_ring_placement"] = ring_variant
+    if launch_variant is not None:
+        if "dt" in launch_variant:
+            variants["launch_placement"] = dict(
+                rate(launch_variant["dt"]), env="BENCH_BIND=none (child process): the calling thread where the "
+                "process was launched", placement=launch_variant.get("placement"),
+                fresh_args=rate(launch_variant["dt_fresh"]))
+        else:
+            variants["launch_placement"] = launch_variant
     out["sync_variants"] = variants
 
     if share:
@@ -1076,7 +1215,8 @@ def main():
         s.synchronize()
         ev_ms = sorted(e0.elapsed_time(e1) for e0, e1 in evs)
         ev_mean_us = sum(ev_ms) / len(ev_ms) * 1e3
-        ns = direct_kernel_ns(lib, step, args.steps, args.warmup)
+        splits = []
+        ns = direct_kernel_ns(lib, step, args.steps, args.warmup, splits)
         if ns is not None:
             us_sorted = sorted(x * 1e-3 for x in ns)
             kernel = ("mpir_tile_SUM_MPIR_HIP_F32 (the synchronous call's kernel, direct AQL dispatch, "
@@ -1115,7 +1255,8 @@ def main():
             "call_mean_us": round(call_mean_us, 2), "kernel_mean_us": round(mean_us, 2),
             "fixed_us": round(fixed, 2), "call_median_minus_kernel_median_us": round(
                 cstats["median_us"] - us_sorted[len(us_sorted) // 2], 2),
-            "kernel_us_for_call_at_0.80": round(alg_bytes / (0.8 * HBM_PEAK_BPS) * 1e6 - fixed, 2)}
+            "kernel_us_for_call_at_0.80": round(alg_bytes / (0.8 * HBM_PEAK_BPS) * 1e6 - fixed, 2),
+            "split_medians": split_medians(splits)}
 
         # ---- configs 2 and 3 (kernel time per synchronous call, same method)
         out["config3_sweep"] = config3_sweep(m, lib, pairs, nbytes, s)
@@ -1157,14 +1298,18 @@ def main():
             dth = time_steps(hstep, hk, 1, sync, barrier, max_over_ranks)
             dtp = time_steps(pstep, hk, 1, sync, barrier, max_over_ranks)
             # the same pageable pages registered with hipHostRegister: how a PiP /
-            # shm segment is pinned in place (SURVEY.md §8d host-inclusive rate)
-            hip = ctypes.CDLL("libamdhip64.so.7")   # the library's own HIP runtime, not torch's bundled copy
+            # shm segment is pinned in place (SURVEY.md §8d host-inclusive rate),
+            # through the library's own HIP runtime (not torch's bundled copy)
+            hip = library_hip_runtime(lib)
             regd = []
-            for arr in (pa, pb):
+            for arr in (pa, pb) if hip is not None else ():
                 if hip.hipHostRegister(ctypes.c_void_p(arr.ctypes.data), ctypes.c_size_t(arr.nbytes), 0) == 0:
                     regd.append(arr)
+            # every rank times the registered loop, or none does: its barrier and
+            # max over ranks are collectives
+            all_regd = max_over_ranks(0.0 if len(regd) == 2 else 1.0) == 0.0
             try:
-                dtr = time_steps(pstep, hk, 1, sync, barrier, max_over_ranks) if len(regd) == 2 else None
+                dtr = time_steps(pstep, hk, 1, sync, barrier, max_over_ranks) if all_regd else None
             finally:
                 for arr in regd:
                     hip.hipHostUnregister(ctypes.c_void_p(arr.ctypes.data))

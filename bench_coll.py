@@ -134,6 +134,36 @@ def expect_scan(xs, rank: int, exclusive: bool = False):
     return acc
 
 
+# the self-check's sizes (main, part 1)
+SELF_N = (1 << 16) + 3          # fp32 allreduce / reduce / scan / exscan
+SELF_RCOUNT = (1 << 17) + 3     # fp16 reduce_scatter_block recvcount: pairwise at every N >= 2
+INT_N = 4099                    # int32 allreduce over RCCL
+
+
+def call_plan(world: int, ar_mib: int = 256, rs_mib: int = 1024, warmup: int = 3, steps: int = 10) -> list:
+    """Every collective main() issues on each rank, in its order, as
+    (call, count, type, op, algorithm[, root]) -- what a rank of this bench
+    asks of RCCL through the C ABI.  tests/test_rccl_sequence_cpu.py replays it
+    against a recording librccl stand-in at N = 2..8 and checks that the ranks'
+    RCCL call sequences match one another (no GPU)."""
+    plan = [("allreduce", SELF_N, "f32", "sum", "ref"),
+            ("reduce_scatter_block", SELF_RCOUNT, "f16", "sum", "ref"),
+            ("reduce", SELF_N, "f32", "sum", "ref", world - 1),
+            ("scan", SELF_N, "f32", "sum", "ref"), ("exscan", SELF_N, "f32", "sum", "ref"),
+            ("allreduce", SELF_N, "f32", "sum", "rccl"),
+            ("reduce_scatter_block", SELF_RCOUNT, "f16", "sum", "rccl"),
+            ("allreduce", INT_N, "i32", "sum", "rccl"),
+            ("allreduce", 8, "f64", "min", "rccl")]             # the flags
+    barrier = ("allreduce", 1, "f64", "sum", "rccl")
+    per_rank = ("allreduce", world, "f64", "sum", "rccl")
+    count = ar_mib * (1 << 20) // 4
+    rc_ = rs_mib * (1 << 20) // 2 // world
+    for call, n, ty in (("allreduce", count, "f32"), ("reduce_scatter_block", rc_, "f16")):
+        for alg in ("rccl", "ref"):
+            plan += [(call, n, ty, "sum", alg)] * warmup + [barrier] + [(call, n, ty, "sum", alg)] * steps + [per_rank]
+    return plan
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=10)
@@ -190,7 +220,7 @@ def main():
 
     # ---- 1. self-check over the real transport (small, deterministic, finite inputs)
     pof2 = world & (world - 1) == 0
-    n = (1 << 16) + 3
+    n = SELF_N
     xs = [np.random.default_rng(77 + r).uniform(-1, 1, n).astype(np.float32) for r in range(world)]
     send = torch.from_numpy(xs[rank].copy()).cuda()
     recv = torch.zeros_like(send)
@@ -200,7 +230,7 @@ def main():
         if pof2 else True
     # large enough that MPICH takes the pairwise algorithm at every N >= 2
     # (p * recvcount * 2 B >= 524288, reduce_scatter_block.c:136-141)
-    rcount = (1 << 17) + 3
+    rcount = SELF_RCOUNT
     hs = [np.random.default_rng(91 + r).uniform(-4, 4, rcount * world).astype(np.float16) for r in range(world)]
     hsend = torch.from_numpy(hs[rank].copy()).cuda()
     hrecv = torch.zeros(rcount, dtype=torch.float16, device="cuda")
@@ -243,12 +273,12 @@ def main():
     g16 = (world - 1) * 2.0 ** -11 / (1 - (world - 1) * 2.0 ** -11)
     # the reference chain rounds to fp16 at every step too: allow both chains' error
     ok_rccl_rs = bool(np.all(np.abs(hr2.cpu().numpy().astype(np.float64) - href) <= 2 * g16 * hmag + 2.0 ** -24))
-    ints = [np.random.default_rng(300 + r).integers(-2 ** 31, 2 ** 31, 4099, dtype=np.int64).astype(np.int32)
+    ints = [np.random.default_rng(300 + r).integers(-2 ** 31, 2 ** 31, INT_N, dtype=np.int64).astype(np.int32)
             for r in range(world)]
     isend = torch.from_numpy(ints[rank].copy()).cuda()
     irecv = torch.zeros_like(isend)
     torch.cuda.synchronize()
-    assert m.allreduce(isend.data_ptr(), irecv.data_ptr(), 4099, m.MPI_INT, SUM, C, RCCL) == 0
+    assert m.allreduce(isend.data_ptr(), irecv.data_ptr(), INT_N, m.MPI_INT, SUM, C, RCCL) == 0
     iwant = np.sum([x.astype(np.int64) for x in ints], axis=0).astype(np.uint32).view(np.int32)
     ok_rccl_int = bool(np.array_equal(irecv.cpu().numpy(), iwant))
     flags = torch.tensor([float(ok_ar), float(ok_rs), float(ok_rd), float(ok_sc), float(ok_ex), float(ok_rccl_ar),

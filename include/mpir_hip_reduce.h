@@ -137,9 +137,10 @@ uint64_t MPIR_Hip_direct_last_kernel_ns(void);
  * 2 ready with every kernarg write made visible by a flush read back before
  * the doorbell -- the queue's dispatch ids are not its packet indices, as
  * under a tool that intercepts queues such as rocprofv3 --kernel-trace;
- * -1..-11 the initialisation step that failed: properties, hsa_init, agents,
+ * -1..-12 the initialisation step that failed: properties, hsa_init, agents,
  * VRAM pool, HDP register, code-object file, code-object load, kernel
- * symbols, kernarg memory, queue, error word; -20 disabled by
+ * symbols, kernarg memory, queue, error word, and (-12) a code object built
+ * from other sources than this library (MPIR_Hip_build_id); -20 disabled by
  * MPIR_CVAR_REDUCE_LOCAL_DISPATCH=hip), and the number of direct calls that
  * first synchronised with work reported pending on the legacy null stream. */
 int MPIR_Hip_direct_state(int dev);
@@ -171,7 +172,19 @@ uint32_t MPIR_Hip_direct_test_write_delay_us(uint32_t us);
  * read-back flushes (MPIR_Hip_direct_state 2) and must still complete
  * (tests/test_direct_prepare_gpu.py). */
 void MPIR_Hip_direct_test_fail_probe(void);
+/* Where the synchronous call's host side runs relative to device `dev`
+ * (diagnostic; bench.py records it per rank): out[0] the calling thread's CPU
+ * (sched_getcpu), out[1] that CPU's NUMA node, out[2] the device's NUMA node
+ * (its PCI function's sysfs numa_node), out[3] the node of the page holding
+ * this thread's completion signal for dev, out[4] the node of the device's
+ * error word; -1 where unknown or not yet created. */
+void MPIR_Hip_direct_placement(int dev, int out[5]);
 int MPIR_Hip_thread_contexts(void);
+
+/* The build id of this library: "src=<hash of csrc/ and include/> tiles=<hash
+ * of the direct path's code object sources> git=<commit>[+dirty]" (Makefile),
+ * so a run can show which sources its binaries came from. */
+const char *MPIR_Hip_build_id(void);
 
 /* Ranks of this job on this node, for sizing the host combine's threads: the
  * node's CPUs are shared by every local rank, and all of them reach the

@@ -48,12 +48,16 @@
 #include <hsa/hsa.h>
 #include <hsa/hsa_ext_amd.h>
 #include <hsa/amd_hsa_signal.h>
+#include <ctype.h>
+#include <dirent.h>
 #include <dlfcn.h>
 #include <immintrin.h>
+#include <sched.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 #include <pthread.h>
+#include <sys/syscall.h>
 #include <time.h>
 #include <unistd.h>
 
@@ -69,6 +73,10 @@
 namespace mpir_hip {
 
 namespace {
+
+#ifndef MPIR_TILES_HASH
+#define MPIR_TILES_HASH "unknown"   // (the Makefile passes the code object's source hash)
+#endif
 
 constexpr int kMaxDirectDev = 64;
 constexpr uint32_t kKargSlotBytes = sizeof(KargSlot);
@@ -413,6 +421,18 @@ void init_dev(int dev, DevState &d) {
     size_t n;
     while ((n = fread(buf, 1, sizeof buf, fp)) > 0) co.insert(co.end(), buf, buf + n);
     fclose(fp);
+    // built from the sources this library was built from (Makefile TILES_HASH,
+    // direct_tiles.hip mpir_tiles_build_id): else the HIP path takes every call
+    d.state = -12;
+    {
+        static const char tag[] = "mpir-tiles-build:" MPIR_TILES_HASH;
+        const std::string bytes(co.begin(), co.end());
+        if (bytes.find(tag) == std::string::npos) {
+            fprintf(stderr, "mpir_hip: %s was not built from this library's sources (want %s); direct dispatch off\n",
+                    path.c_str(), tag);
+            return;
+        }
+    }
     d.state = -7;
     hsa_code_object_reader_t rd;
     hsa_executable_t exe;
@@ -621,6 +641,130 @@ struct DirectSignals {
 };
 thread_local DirectSignals t_sig;
 
+// ---- placement: where the synchronous call's host side runs relative to the
+// device.  The call's host-memory traffic is the doorbell write (MMIO to the
+// device's BAR), the completion signal the CP writes and the host polls, and
+// the error word read once per call; everything else (AQL ring, kernargs) sits
+// in VRAM.
+namespace {
+// NUMA node of the page holding p (-1 if unknown): move_pages without target
+// nodes only reports where each page lives
+int page_node(const void *p) {
+    void *pg = reinterpret_cast<void *>(reinterpret_cast<uintptr_t>(p) & ~(uintptr_t)4095);
+    int status = -1;
+    if (syscall(SYS_move_pages, 0, 1UL, &pg, nullptr, &status, 0) == 0 && status >= 0) return status;
+    // driver mappings (the runtime's signal pages) answer no page: the node
+    // /proc/self/numa_maps gives their mapping (its "N<node>=<pages>" fields,
+    // the node holding most of them)
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+    uintptr_t vma = 0;
+    bool found = false;
+    char line[4096];
+    if (FILE *m = fopen("/proc/self/maps", "r")) {
+        while (!found && fgets(line, sizeof line, m)) {
+            char *dash = nullptr;
+            const uintptr_t lo = (uintptr_t)strtoull(line, &dash, 16);
+            const uintptr_t hi = dash && *dash == '-' ? (uintptr_t)strtoull(dash + 1, nullptr, 16) : 0;
+            if (lo <= a && a < hi) {
+                vma = lo;
+                found = true;
+            }
+        }
+        fclose(m);
+    }
+    FILE *f = found ? fopen("/proc/self/numa_maps", "r") : nullptr;
+    if (!f) return -1;
+    int node = -1;
+    while (fgets(line, sizeof line, f)) {
+        if ((uintptr_t)strtoull(line, nullptr, 16) != vma) continue;
+        long most = 0;
+        for (char *t = strstr(line, " N"); t; t = strstr(t + 1, " N")) {
+            int n = -1;
+            long pages = 0;
+            if (sscanf(t, " N%d=%ld", &n, &pages) == 2 && pages > most) {
+                most = pages;
+                node = n;
+            }
+        }
+    }
+    fclose(f);
+    return node;
+}
+// NUMA node of a CPU: the nodeN entry of its sysfs directory
+int cpu_node(int cpu) {
+    if (cpu < 0) return -1;
+    char path[64];
+    snprintf(path, sizeof path, "/sys/devices/system/cpu/cpu%d", cpu);
+    DIR *d = opendir(path);
+    if (!d) return -1;
+    int node = -1;
+    for (struct dirent *e; (e = readdir(d)) != nullptr;)
+        if (!strncmp(e->d_name, "node", 4) && e->d_name[4] >= '0' && e->d_name[4] <= '9') {
+            node = atoi(e->d_name + 4);
+            break;
+        }
+    closedir(d);
+    return node;
+}
+// NUMA node of HIP device dev's PCI function (-1: unknown or no NUMA)
+int device_node(int dev) {
+    char bus[64] = {};
+    if (hipDeviceGetPCIBusId(bus, (int)sizeof bus, dev) != hipSuccess) {
+        (void)hipGetLastError();
+        return -1;
+    }
+    for (char *c = bus; *c; ++c) *c = (char)tolower((unsigned char)*c);
+    char path[128];
+    snprintf(path, sizeof path, "/sys/bus/pci/devices/%s/numa_node", bus);
+    FILE *f = fopen(path, "r");
+    if (!f) return -1;
+    int node = -1;
+    if (fscanf(f, "%d", &node) != 1) node = -1;
+    fclose(f);
+    return node;
+}
+}  // namespace
+
+// out: the calling thread's CPU, that CPU's NUMA node, device dev's NUMA node,
+// the node of the page holding this thread's completion signal for dev (-1
+// before its first direct call, or unknown), the node of the device's error
+// word (-1 before the direct path initialised)
+void direct_placement(int dev, int out[5]) {
+    const int cpu = sched_getcpu();
+    out[0] = cpu;
+    out[1] = cpu_node(cpu);
+    out[2] = dev >= 0 && dev < kMaxDirectDev ? device_node(dev) : -1;
+    out[3] = dev >= 0 && dev < kMaxDirectDev && t_sig.have[dev]
+                 ? page_node(reinterpret_cast<const void *>((uintptr_t)t_sig.sig[dev].handle))
+                 : -1;
+    out[4] = dev >= 0 && dev < kMaxDirectDev && g_dev[dev].err ? page_node((const void *)g_dev[dev].err) : -1;
+}
+
+// How the caller waits for the completion signal (A/B knobs for
+// tools/placement_ab.py; the defaults are the product's):
+//   MPIR_CVAR_REDUCE_LOCAL_POLL_DELAY_US  spin on the clock, without reading
+//       the signal, this long after the doorbell before polling it (0);
+//   MPIR_CVAR_REDUCE_LOCAL_POLL_FLUSH=1   clflush the signal's line once the
+//       call has seen it, so no CPU cache holds it when the CP next writes it (0).
+struct PollCfg {
+    uint64_t delay_ns = 0;
+    bool flush = false;
+};
+const PollCfg &poll_cfg() {
+    static const PollCfg c = [] {
+        PollCfg v;
+        if (const char *e = getenv("MPIR_CVAR_REDUCE_LOCAL_POLL_DELAY_US")) v.delay_ns = (uint64_t)atol(e) * 1000;
+        if (const char *e = getenv("MPIR_CVAR_REDUCE_LOCAL_POLL_FLUSH")) v.flush = atoi(e) != 0;
+        return v;
+    }();
+    return c;
+}
+static inline uint64_t mono_ns() {
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return (uint64_t)ts.tv_sec * 1000000000ull + (uint64_t)ts.tv_nsec;
+}
+
 // 1: dispatched and completed (rc set); 0: not applicable, use the HIP path.
 // `p` is plan_reduce's launch plan of the call (padding bytes zero).
 int direct_reduce(int dev, int op, int elem, const ReducePlan &p, int *rc) {
@@ -652,6 +796,7 @@ int direct_reduce(int dev, int op, int elem, const ReducePlan &p, int *rc) {
     }
     hsa_signal_t sig;
     if (!t_sig.get(dev, &sig)) return 0;
+    uint64_t t_rung = 0;
     const uint32_t groups = (uint32_t)p.groups;
     const unsigned char *ka = p.args;
     const uint32_t kn = p.arg_bytes;
@@ -766,6 +911,7 @@ int direct_reduce(int dev, int op, int elem, const ReducePlan &p, int *rc) {
                        checked && groups < kMinCheckedGroups ? kMinCheckedGroups : groups);
         if (prof) th1 = sys_ts();
         hsa_signal_store_screlease(q->doorbell_signal, idx);
+        if (poll_cfg().delay_ns) t_rung = mono_ns();
         if (late) {
             const auto t_end = std::chrono::steady_clock::now() + std::chrono::microseconds(late);
             while (std::chrono::steady_clock::now() < t_end) _mm_pause();
@@ -776,6 +922,8 @@ int direct_reduce(int dev, int op, int elem, const ReducePlan &p, int *rc) {
             *d.hdp = 1u;
         }
     }
+    if (t_rung)
+        while (mono_ns() - t_rung < poll_cfg().delay_ns) _mm_pause();
     for (uint64_t it = 1; hsa_signal_load_scacquire(sig) != 0; ++it) {
         if ((it & 0xFFFF) == 0 && d.queue_error.load(std::memory_order_relaxed)) {
             *rc = MPIR_HIP_ERUNTIME;
@@ -783,6 +931,7 @@ int direct_reduce(int dev, int op, int elem, const ReducePlan &p, int *rc) {
         }
         _mm_pause();
     }
+    if (poll_cfg().flush) _mm_clflush(reinterpret_cast<const char *>((uintptr_t)sig.handle) + 8);
     if (__builtin_expect(*d.err != 0, 0)) {
         // a workgroup never saw its arguments land (direct_tiles.hip
         // checked_args) and combined nothing: this call fails, and the path is

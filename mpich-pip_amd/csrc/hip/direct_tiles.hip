@@ -134,6 +134,15 @@ extern "C" __global__ __launch_bounds__(64) void mpir_probe_dispatch_id(KargSlot
                            __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// The hash of this code object's sources (Makefile TILES_HASH), as bytes in
+// the file: direct_dispatch.hip loads the code object only if it matches the
+// hash libmpir_hip.so was built with, so a stale .hsaco beside a newer library
+// leaves the direct path off instead of running other kernel bodies.
+#ifndef MPIR_TILES_HASH
+#define MPIR_TILES_HASH "unknown"
+#endif
+extern "C" __attribute__((used)) __device__ const char mpir_tiles_build_id[] = "mpir-tiles-build:" MPIR_TILES_HASH;
+
 // unchecked: the plan's argument words as they stand, all loaded up front in
 // one statement (left to itself the compiler sinks the words the tile reads
 // after its early exit into a second, dependent scalar round trip)

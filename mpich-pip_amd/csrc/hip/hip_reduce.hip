@@ -18,6 +18,7 @@
 #include <atomic>
 #include <condition_variable>
 #include <mutex>
+#include <string>
 #include <thread>
 #include <vector>
 
@@ -47,6 +48,7 @@ uint64_t direct_busy_skips();
 uint64_t direct_kernarg_writes();
 uint32_t direct_test_write_delay_us(uint32_t us);
 void direct_test_fail_probe();
+void direct_placement(int dev, int out[5]);
 Entry g_table[MPIR_HIP_NOPS][MPIR_HIP_NELEMS];
 multi_fn g_multi[MPIR_HIP_NOPS][MPIR_HIP_NELEMS][2][kMultiMaxP - 1];
 
@@ -383,36 +385,91 @@ int local_ranks() {
 // at the first call, so MPIR_Hip_set_local_ranks() acts before the first host
 // combine)
 int parse_cpulist(const char *path, std::vector<int> &out);
-// The CPUs the job's ranks can share: the cgroup's cpuset (a container pinned
-// to 16 of the host's 256 CPUs gives every unbound rank that same 16-CPU mask),
-// else the online CPUs
-int online_cpus() {
-    for (const char *path : {"/sys/fs/cgroup/cpuset.cpus.effective", "/sys/fs/cgroup/cpuset/cpuset.effective_cpus"}) {
-        std::vector<int> cpus;
-        if (parse_cpulist(path, cpus) == 0 && !cpus.empty()) return (int)cpus.size();
-    }
-    const long n = sysconf(_SC_NPROCESSORS_ONLN);
-    return n >= 1 ? (int)n : 1;
-}
-// the cgroup's CPU quota in CPUs (v2 cpu.max "quota period", v1 cfs_quota_us /
-// cfs_period_us), 0 if none
-int cgroup_quota_cpus() {
-    long quota = -1, period = 0;
-    if (FILE *f = fopen("/sys/fs/cgroup/cpu.max", "r")) {
-        char q[32];
-        if (fscanf(f, "%31s %ld", q, &period) == 2 && strcmp(q, "max") != 0) quota = atol(q);
-        fclose(f);
-    } else if (FILE *fq = fopen("/sys/fs/cgroup/cpu/cpu.cfs_quota_us", "r")) {
-        if (fscanf(fq, "%ld", &quota) != 1) quota = -1;
-        fclose(fq);
-        if (FILE *fp = fopen("/sys/fs/cgroup/cpu/cpu.cfs_period_us", "r")) {
-            if (fscanf(fp, "%ld", &period) != 1) period = 0;
-            fclose(fp);
+// This process's own cgroup, as /proc/self/cgroup names it: the v2 path ("0::")
+// or the v1 path of `controller`; "" if the file or the entry is missing.  The
+// cgroup files are read there and up its ancestors (without a
+// cgroup namespace -- Slurm on bare metal -- the mount's root files describe
+// the whole node, not this job).
+std::string own_cgroup(const char *controller) {
+    FILE *f = fopen("/proc/self/cgroup", "r");
+    if (!f) return "";
+    char line[1024];
+    std::string v2, v1;
+    while (fgets(line, sizeof line, f)) {
+        line[strcspn(line, "\n")] = 0;
+        char *c1 = strchr(line, ':');
+        char *c2 = c1 ? strchr(c1 + 1, ':') : nullptr;
+        if (!c2) continue;
+        *c2 = 0;
+        const char *ctrls = c1 + 1, *path = c2 + 1;
+        if (!strncmp(line, "0", 2) && !*ctrls) v2 = path;
+        for (const char *t = ctrls; *t;) {                  // "cpu,cpuacct"
+            const size_t n = strcspn(t, ",");
+            if (n == strlen(controller) && !strncmp(t, controller, n)) v1 = path;
+            t += n + (t[n] == ',');
         }
     }
-    if (quota <= 0 || period <= 0) return 0;
-    const long v = (quota + period - 1) / period;
-    return v >= 1 && v < (1L << 20) ? (int)v : 0;
+    fclose(f);
+    return !v1.empty() ? "/sys/fs/cgroup/" + std::string(controller) + v1 : (!v2.empty() ? "/sys/fs/cgroup" + v2 : "");
+}
+// dir and its ancestors up to the mount point (inclusive), innermost first
+std::vector<std::string> cgroup_chain(const std::string &dir, const char *mount) {
+    std::vector<std::string> out;
+    std::string d = dir;
+    while (d.size() > strlen(mount) && d.compare(0, strlen(mount), mount) == 0) {
+        while (d.size() > 1 && d.back() == '/') d.pop_back();
+        out.push_back(d);
+        d = d.substr(0, d.rfind('/'));
+    }
+    out.push_back(mount);
+    return out;
+}
+// The CPUs the job's ranks can share: this process's cgroup cpuset (a
+// container pinned to 16 of the host's 256 CPUs gives every unbound rank that
+// same 16-CPU mask), read at its own cgroup or the nearest ancestor that has
+// one.  If no cpuset can be found, `mask` (this process's affinity): the L
+// local ranks are then taken to share it, the conservative reading.
+int online_cpus(int mask) {
+    const std::string v1 = own_cgroup("cpuset");
+    const bool is_v1 = v1.compare(0, 22, "/sys/fs/cgroup/cpuset/") == 0 || v1 == "/sys/fs/cgroup/cpuset";
+    const char *mount = is_v1 ? "/sys/fs/cgroup/cpuset" : "/sys/fs/cgroup";
+    const char *file = is_v1 ? "/cpuset.effective_cpus" : "/cpuset.cpus.effective";
+    if (!v1.empty())
+        for (const std::string &d : cgroup_chain(v1, mount)) {
+            std::vector<int> cpus;
+            if (parse_cpulist((d + file).c_str(), cpus) == 0 && !cpus.empty()) return (int)cpus.size();
+        }
+    return mask >= 1 ? mask : 1;
+}
+// the cgroup's CPU quota in CPUs (v2 cpu.max "quota period", v1 cfs_quota_us /
+// cfs_period_us) -- the smallest along this process's cgroup and its
+// ancestors -- 0 if none
+int cgroup_quota_cpus() {
+    const std::string own = own_cgroup("cpu");
+    if (own.empty()) return 0;
+    const bool is_v1 = own.compare(0, 19, "/sys/fs/cgroup/cpu/") == 0 || own == "/sys/fs/cgroup/cpu";
+    long best = 0;
+    for (const std::string &d : cgroup_chain(own, is_v1 ? "/sys/fs/cgroup/cpu" : "/sys/fs/cgroup")) {
+        long quota = -1, period = 0;
+        if (!is_v1) {
+            if (FILE *f = fopen((d + "/cpu.max").c_str(), "r")) {
+                char q[32];
+                if (fscanf(f, "%31s %ld", q, &period) == 2 && strcmp(q, "max") != 0) quota = atol(q);
+                fclose(f);
+            }
+        } else if (FILE *fq = fopen((d + "/cpu.cfs_quota_us").c_str(), "r")) {
+            if (fscanf(fq, "%ld", &quota) != 1) quota = -1;
+            fclose(fq);
+            if (FILE *fp = fopen((d + "/cpu.cfs_period_us").c_str(), "r")) {
+                if (fscanf(fp, "%ld", &period) != 1) period = 0;
+                fclose(fp);
+            }
+        }
+        if (quota <= 0 || period <= 0) continue;
+        const long v = (quota + period - 1) / period;
+        if (v >= 1 && v < (1L << 20) && (best == 0 || v < best)) best = v;
+    }
+    return (int)best;
 }
 int share_threads(int mask, int online, int quota, int L) {
     if (L < 1) L = 1;
@@ -437,7 +494,7 @@ int pool_threads() {
         }
         cpu_set_t set;
         const int mask = sched_getaffinity(0, sizeof set, &set) == 0 ? CPU_COUNT(&set) : 1;
-        return share_threads(mask, online_cpus(), cgroup_quota_cpus(), local_ranks());
+        return share_threads(mask, online_cpus(mask), cgroup_quota_cpus(), local_ranks());
     }();
     return n;
 }
@@ -788,7 +845,13 @@ bool cpu_agent(hsa_agent_t a) {
 // (`reuse`, verdict_reusable below: within both the mixed slot's and the host
 // combine's limits, where pinned and pageable differ only in the null-stream
 // ordering) take a kept verdict; a larger call asks HIP again and refreshes it.
-Loc classify(const void *p, int *dev, bool reuse = true) {
+// And because the page, not the buffer, keys the table (a registered buffer
+// may share its first page with a pageable one classified earlier, or be
+// registered after its verdict was kept: ADVICE r5), a call that took a kept
+// host verdict (`*kept`) orders its host reads after the null stream whatever
+// the verdict says -- the one thing pinned and pageable differ in there.
+Loc classify(const void *p, int *dev, bool reuse = true, bool *kept = nullptr) {
+    if (kept) *kept = false;
     if (!gpu_runtime_started()) return LOC_HOST;
     hsa_amd_pointer_info_t info;
     info.size = sizeof info;
@@ -809,6 +872,7 @@ Loc classify(const void *p, int *dev, bool reuse = true) {
     HostVerdict &v = ctx().verdict[(page ^ (page >> 7)) & (kVerdicts - 1)];
     if (reuse && v.page == page) {
         *dev = v.dev;
+        if (kept) *kept = true;
         return (Loc)v.loc;
     }
     const Loc l = classify_hip(p, dev);
@@ -854,9 +918,10 @@ int order_after_null_stream() {
 // have filled through that device's null stream while another was current
 // (ADVICE r3): that device's null stream, then the caller's device back
 int order_after_null_stream_of(int dev) {
+    if (dev < 0) return order_after_null_stream();      // the caller's current device
     int cur = 0;
     HIPCHK(hipGetDevice(&cur));
-    if (dev < 0 || dev == cur) return order_after_null_stream();
+    if (dev == cur) return order_after_null_stream();
     HIPCHK(hipSetDevice(dev));
     const int rc = order_after_null_stream();
     (void)hipSetDevice(cur);
@@ -1029,6 +1094,7 @@ uint64_t MPIR_Hip_direct_busy_skips(void) { return direct_busy_skips(); }
 uint64_t MPIR_Hip_direct_kernarg_writes(void) { return direct_kernarg_writes(); }
 uint32_t MPIR_Hip_direct_test_write_delay_us(uint32_t us) { return direct_test_write_delay_us(us); }
 void MPIR_Hip_direct_test_fail_probe(void) { direct_test_fail_probe(); }
+void MPIR_Hip_direct_placement(int dev, int out[5]) { direct_placement(dev, out); }
 
 int MPIR_Hip_set_local_ranks(int n) {
     return g_local_ranks.exchange(n > 0 ? n : 0);
@@ -1136,9 +1202,16 @@ int MPIR_Hip_reduce(const void *inbuf, void *inoutbuf, uint64_t count, int op, i
     ctx().err[0] = 0;
     launch_fn fn = g_table[op][elem].fn;
     int din = -1, dio = -1;
+    bool kin = false, kio = false;
     const bool reuse = verdict_reusable(count * esz);
-    const Loc lin = classify(inbuf, &din, reuse);
-    const Loc lio = classify(inoutbuf, &dio, reuse);
+    const Loc lin = classify(inbuf, &din, reuse, &kin);
+    const Loc lio = classify(inoutbuf, &dio, reuse, &kio);
+    // a host operand the host reads below waits for the null stream if it is
+    // pinned, or if its verdict was a kept one (classify: it may be stale)
+    const bool order_in = lin == LOC_PINNED || (lin == LOC_HOST && kin);
+    const bool order_io = lio == LOC_PINNED || (lio == LOC_HOST && kio);
+    // the device whose null stream that is: the pinned buffer's, else the caller's
+    const int odin = lin == LOC_PINNED ? din : -1, odio = lio == LOC_PINNED ? dio : -1;
 
     // ---- fast path: both operands device-resident on one device ----------
     if (lin == LOC_DEVICE && lio == LOC_DEVICE && din == dio)
@@ -1149,9 +1222,8 @@ int MPIR_Hip_reduce(const void *inbuf, void *inoutbuf, uint64_t count, int op, i
     if (lin != LOC_DEVICE && lio != LOC_DEVICE && (count * esz <= host_max_bytes() || device_count() == 0) &&
         g_table[op][elem].host) {
         int rc = MPIR_HIP_OK;
-        if (lin == LOC_PINNED) rc = order_after_null_stream_of(din);
-        if (rc == MPIR_HIP_OK && lio == LOC_PINNED && !(lin == LOC_PINNED && din == dio))
-            rc = order_after_null_stream_of(dio);
+        if (order_in) rc = order_after_null_stream_of(odin);
+        if (rc == MPIR_HIP_OK && order_io && !(order_in && odin == odio)) rc = order_after_null_stream_of(odio);
         if (rc != MPIR_HIP_OK) return rc;
         return host_combine(op, elem, inbuf, inoutbuf, count * esz / unit, unit);
     }
@@ -1166,14 +1238,14 @@ int MPIR_Hip_reduce(const void *inbuf, void *inoutbuf, uint64_t count, int op, i
         const uintptr_t adev = reinterpret_cast<uintptr_t>(lin == LOC_DEVICE ? inbuf : (const void *)inoutbuf);
         char *slot = nullptr;
         int rc = MPIR_HIP_OK;
-        if (lin == LOC_PINNED || lio == LOC_PINNED) {
+        if (lin == LOC_DEVICE ? order_io : order_in) {
             // the host operand is read (copied into the slot) before device_call's
             // own null-stream check: order it first, after the null stream of the
-            // device that owns the pinned buffer and of the device
-            // the kernel runs on
-            const int pdev = lin == LOC_PINNED ? din : dio;
+            // device that owns the pinned buffer (the caller's for a
+            // kept pageable verdict) and of the device the kernel runs on
+            const int pdev = lin == LOC_DEVICE ? odio : odin;
             rc = order_after_null_stream_of(pdev);
-            if (rc == MPIR_HIP_OK && pdev != dev) rc = order_after_null_stream_of(dev);
+            if (rc == MPIR_HIP_OK && pdev >= 0 && pdev != dev) rc = order_after_null_stream_of(dev);
             if (rc != MPIR_HIP_OK) return rc;
         }
         rc = get_zc(dev, (size_t)bytes + 256, &slot);

@@ -743,7 +743,7 @@ constexpr int multi_cap_bytes() {
     // and cap, P = 3 P = 4's: with the operands in one staging slab at
     // stage_stride() apart, as the collectives lay them, 1024 x 1 at one per CU
     // runs CHAIN5-7 0.765-0.773 against 0.749-0.762 for 256 x 4 at three per CU,
-    // and CHAIN3 0.779 against 0.816 (tools/chain_shape.hip chainslab,
+    // and CHAIN3 0.779 against 0.816 (tools/archive/chain_shape.hip chainslab,
     // profiles/r05/chainslab_shape.log).  (With one allocation per operand the
     // order reverses, also for P = 8 below 128 MiB: chain_shape.log,
     // p8_shape*.log against slab_shape.log; the library follows its collectives.)
@@ -881,7 +881,7 @@ hipError_t launch_combine_p(const void *const *ins, void *out_, uint64_t count, 
     // 0.78-0.80 (2 vectors: 0.72-0.74); P = 2 with 4 vectors per lane 0.74-0.76
     // P = 2 over blocks of 256 MiB or more (config 5's 2 x 512 MiB at 2 ranks) on
     // 1024 x 1, uncapped: 0.798-0.808 against 0.784-0.788 for 256 x 4 in the
-    // staging slab; over 128 MiB the two tie (tools/chain_shape.hip p2slab,
+    // staging slab; over 128 MiB the two tie (tools/archive/chain_shape.hip p2slab,
     // profiles/r05/p2slab*.log)
     if constexpr (P == 2) {
         if (count * sizeof(T) >= (256ull << 20))

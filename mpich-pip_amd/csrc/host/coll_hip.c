@@ -63,13 +63,18 @@ static pthread_mutex_t rccl_lock = PTHREAD_MUTEX_INITIALIZER;
 static int rccl_load(void)
 {
     static const char *names[] = { "librccl.so.1", "/opt/rocm/lib/librccl.so.1", "librccl.so" };
+    /* TEST ONLY: a stand-in library that records the calls
+     * (tests/progs/rccl_stub.c, tests/test_rccl_sequence_cpu.py) */
+    const char *test_lib = getenv("MPIR_TEST_RCCL_LIBRARY");
     size_t i;
     pthread_mutex_lock(&rccl_lock);
     if (rccl.loaded) {
         pthread_mutex_unlock(&rccl_lock);
         return rccl.loaded > 0;
     }
-    for (i = 0; i < sizeof(names) / sizeof(names[0]) && !rccl.so; i++)
+    if (test_lib && *test_lib)
+        rccl.so = dlopen(test_lib, RTLD_NOW | RTLD_GLOBAL);
+    for (i = 0; i < sizeof(names) / sizeof(names[0]) && !rccl.so && !(test_lib && *test_lib); i++)
         rccl.so = dlopen(names[i], RTLD_NOW | RTLD_GLOBAL);
     if (rccl.so) {
 #define SYM(f, n) *(void **) (&rccl.f) = dlsym(rccl.so, n)
@@ -353,7 +358,7 @@ static int group_exchange(struct MPIX_Hip_comm_s *c, const xfer_t *sends, int ns
  * skew depends on the block size (the address bits the blocks themselves set):
  * around 128 MiB blocks (config 5's 8 x 128 MiB CHAIN8) 6400 B ran 1.3-4.5
  * points above 4352 B in seven sweeps on five boxes, at 32 / 64 MiB 0.3-1 point
- * below it, at 256 MiB within a point (tools/fold_skew.hip, chain_shape.hip
+ * below it, at 256 MiB within a point (tools/archive/fold_skew.hip, chain_shape.hip
  * slabskew; profiles/r05/fold_skew*.log, slabskew.log).  The skew keeps the
  * 256 B alignment (fused kernels need the operands equal mod 16). */
 static size_t stage_stride(size_t bytes)

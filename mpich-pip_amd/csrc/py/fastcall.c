@@ -91,8 +91,11 @@ static PyObject *fc_reduce_local_loop(PyObject *self, PyObject *const *args, Py_
      * takes sets[i % m] */
     m = n < k ? n : k;
     sets = PyMem_Malloc(sizeof(*sets) * (size_t) (m ? m : 1));
-    if (!sets)
+    if (!sets) {
+        if (stamps)
+            PyBuffer_Release(&view);
         return PyErr_NoMemory();
+    }
     for (i = 0; i < m; i++) {
         PyObject *t = PyTuple_GET_ITEM(args[0], (start + i) % n);
         long count;

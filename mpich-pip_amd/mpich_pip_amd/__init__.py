@@ -121,7 +121,8 @@ EXPORTED_SYMBOLS = [
     "MPIR_Hip_pointer_kind", "MPIR_Hip_memcpy", "MPIR_Hip_error_string", "MPIR_Hip_device_count", "MPIR_Hip_thread_contexts",
     "MPIR_Hip_host_max_bytes", "MPIR_Hip_set_host_max_bytes", "MPIR_Hip_mixed_max_bytes", "MPIR_Hip_direct_dispatches", "MPIR_Hip_direct_profile",
     "MPIR_Hip_direct_last_kernel_ns", "MPIR_Hip_direct_state", "MPIR_Hip_direct_busy_skips",
-    "MPIR_Hip_direct_last_split", "MPIR_Hip_direct_kernarg_writes",
+    "MPIR_Hip_direct_last_split", "MPIR_Hip_direct_kernarg_writes", "MPIR_Hip_direct_placement", "MPIR_Hip_build_id",
+    "MPIR_Hip_direct_prepare", "MPIR_Hip_set_local_ranks", "MPIR_Hip_host_threads",
     # runtime subset for config 1 (include/mpi_pip.h)
     "MPI_Init", "MPI_Initialized", "MPI_Finalize", "MPI_Finalized", "MPI_Abort", "MPI_Comm_size",
     "MPI_Comm_rank", "MPI_Get_processor_name", "MPI_Wtime", "MPI_Wtick", "MPI_Barrier", "MPI_Bcast",
@@ -203,6 +204,15 @@ def load(path: str | None = None) -> ctypes.CDLL:
     lib.MPIR_Hip_direct_kernarg_writes.restype = ctypes.c_uint64
     lib.MPIR_Hip_direct_last_split.argtypes = [ctypes.POINTER(ctypes.c_uint64)]
     lib.MPIR_Hip_direct_last_split.restype = None
+    lib.MPIR_Hip_direct_placement.argtypes = [i32, ctypes.POINTER(i32)]
+    lib.MPIR_Hip_direct_placement.restype = None
+    lib.MPIR_Hip_direct_prepare.argtypes = [i32]
+    lib.MPIR_Hip_direct_prepare.restype = i32
+    lib.MPIR_Hip_set_local_ranks.argtypes = [i32]
+    lib.MPIR_Hip_set_local_ranks.restype = i32
+    lib.MPIR_Hip_host_threads.argtypes = []
+    lib.MPIR_Hip_host_threads.restype = i32
+    lib.MPIR_Hip_build_id.restype = ctypes.c_char_p
     lib.MPIR_Hip_error_string.restype = ctypes.c_char_p
     lib.MPIR_Hip_pointer_kind.argtypes = [vp, ctypes.c_uint64]
     lib.MPIR_Hip_pointer_kind.restype = i32
@@ -213,6 +223,20 @@ def load(path: str | None = None) -> ctypes.CDLL:
     if path is None:
         _lib = lib
     return lib
+
+
+def build_id() -> str:
+    """MPIR_Hip_build_id: the source hashes and commit the library was built from."""
+    return load().MPIR_Hip_build_id().decode()
+
+
+def placement(dev: int = 0) -> dict:
+    """MPIR_Hip_direct_placement for the calling thread: its CPU and NUMA node,
+    device `dev`'s node, and the nodes of this thread's completion signal and of
+    the device's error word (-1 where unknown or not yet created)."""
+    out = (ctypes.c_int * 5)()
+    load().MPIR_Hip_direct_placement(dev, out)
+    return {"cpu": out[0], "cpu_node": out[1], "gpu_node": out[2], "signal_node": out[3], "error_word_node": out[4]}
 
 
 def error_class(code: int) -> int:

@@ -297,3 +297,69 @@ def test_registration_after_kept_verdict(mpi, orc, hip):
     assert not t.is_alive(), "case hung"
     if err:
         raise err[0]
+
+
+def test_kept_pageable_verdict_orders_after_null_stream(mpi, orc, hip):
+    """kept host verdicts are keyed by the 4 KiB page, and
+    a registered buffer may start in the page of a pageable buffer classified
+    earlier.  Here the thread first reduces a pageable buffer A (its verdict
+    kept), then B = A + 2048 B is registered with hipHostRegister and filled
+    by a null-stream hipMemcpyAsync queued behind a 512 MiB device copy, and a
+    small host-host MPI_Reduce_local(C, B) follows at once.  B's page answers
+    with A's kept pageable verdict; the call must still wait for the null
+    stream before reading B (hip_reduce.hip classify `kept`), so B ends as
+    copied + C, bit-exact against the oracle."""
+    lib = mpi.load()
+    err = []
+    n = 16
+
+    def body():
+        ks = Kinds(hip)
+        try:
+            region = np.zeros(NB + 3 * 4096, np.uint8)
+            base = (region.ctypes.data + 4095) & ~4095
+            a_addr, b_addr = base, base + 2048
+            va = np.frombuffer((ctypes.c_char * 64).from_address(a_addr), np.float32)
+            vb = np.frombuffer((ctypes.c_char * 64).from_address(b_addr), np.float32)
+            c = np.linspace(-1, 1, n).astype(np.float32)
+            # A (pageable) reduced small: this page's pageable verdict is kept
+            va[:] = 1.0
+            rc = lib.MPI_Reduce_local(ctypes.c_void_p(c.ctypes.data), ctypes.c_void_p(a_addr), n,
+                                      mpi.MPI_FLOAT, mpi.MPI_SUM)
+            assert rc == 0, mpi.error_string(rc)
+            assert lib.MPIR_Hip_pointer_kind(ctypes.c_void_p(b_addr), 64) == 0      # the kept verdict answers
+            _ok(hip.hipHostRegister(ctypes.c_void_p(b_addr), ctypes.c_size_t(NB), 0), "hipHostRegister")
+            try:
+                big = 512 << 20
+                s0, s1 = ctypes.c_void_p(), ctypes.c_void_p()
+                _ok(hip.hipMalloc(ctypes.byref(s0), ctypes.c_size_t(big)), "hipMalloc")
+                _ok(hip.hipMalloc(ctypes.byref(s1), ctypes.c_size_t(big)), "hipMalloc")
+                ks.frees += [("hipFree", s0.value), ("hipFree", s1.value)]
+                src = np.arange(n, dtype=np.float32) + 100.0
+                dsrc = ks.device()
+                _ok(hip.hipMemcpy(ctypes.c_void_p(dsrc), ctypes.c_void_p(src.ctypes.data), ctypes.c_size_t(64), 1),
+                    "H2D")
+                vb[:] = -7.0
+                # null stream: a long device copy, then the D2H fill of B (registered: DMA, asynchronous)
+                _ok(hip.hipMemcpyAsync(s1, s0, ctypes.c_size_t(big), 3, None), "D2D")
+                _ok(hip.hipMemcpyAsync(ctypes.c_void_p(b_addr), ctypes.c_void_p(dsrc), ctypes.c_size_t(64), 2, None),
+                    "D2H")
+                rc = lib.MPI_Reduce_local(ctypes.c_void_p(c.ctypes.data), ctypes.c_void_p(b_addr), n,
+                                          mpi.MPI_FLOAT, mpi.MPI_SUM)
+                assert rc == 0, mpi.error_string(rc)
+                _ok(hip.hipDeviceSynchronize(), "sync")
+                want = src.copy()
+                assert orc.reduce_local(c.copy(), want, n, mpi.MPI_FLOAT, mpi.MPI_SUM) == 0
+                assert np.array_equal(vb.view(np.uint32), want.view(np.uint32)), (vb, want)
+            finally:
+                _ok(hip.hipHostUnregister(ctypes.c_void_p(b_addr)), "hipHostUnregister")
+        except BaseException as e:      # noqa: BLE001
+            err.append(e)
+        finally:
+            ks.close()
+    t = threading.Thread(target=body)
+    t.start()
+    t.join(120)
+    assert not t.is_alive(), "case hung"
+    if err:
+        raise err[0]

@@ -4,7 +4,7 @@ running output).  Reduce_scatter_block's pairwise schedule at p ranks folds p
 blocks of 1 GiB / p (fp16, config 5's sendbuf) in this order
 (reduce_scatter_block_intra_pairwise.c:97-134).
 
-    python tools/chain_np2.py [rounds = 9]
+    python tools/archive/chain_np2.py [rounds = 9]
 
 Both forms through MPIX_Reduce_local_multi on one stream (the chunks are the
 library's own P = 4 / P = 2 fused kernels, exactly the calls the old loop

@@ -4,8 +4,8 @@
 // in P = 4's, 256 threads x 4 vectors under a 53 KiB cap = three per CU).
 //
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off \
-//         -Impich-pip_amd/csrc/hip -o tools/chain_shape tools/chain_shape.hip
-//   tools/chain_shape [rounds = 9] [chain | chainslab | chainskew | p2slab | p4slab | tree | p8 | slab | slabskew]
+//         -Impich-pip_amd/csrc/hip -o tools/archive/chain_shape tools/archive/chain_shape.hip
+//   tools/archive/chain_shape [rounds = 9] [chain | chainslab | chainskew | p2slab | p4slab | tree | p8 | slab | slabskew]
 //
 // fp16 SUM CHAIN over p blocks of 1 GiB / p (config 5's sendbuf at p ranks),
 // two operand sets alternated, HIP events over batches of 10 back-to-back

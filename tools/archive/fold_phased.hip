@@ -2,8 +2,8 @@
 // read/write turnarounds?  (DESIGN.md §(f), "Where the fold's time goes".)
 //
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off \
-//         -Impich-pip_amd/csrc/hip -o tools/fold_phased tools/fold_phased.hip
-//   tools/fold_phased [rounds = 10]
+//         -Impich-pip_amd/csrc/hip -o tools/archive/fold_phased tools/archive/fold_phased.hip
+//   tools/archive/fold_phased [rounds = 10]
 //
 // The product's fold mixes its eight read streams with its write stream all
 // the time.  Here one workgroup per CU (1024 threads) folds K tiles per phase

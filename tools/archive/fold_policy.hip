@@ -5,8 +5,8 @@
 // gap every 4 loads, 96 KiB LDS reservation = one workgroup per CU).
 //
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off \
-//         -Impich-pip_amd/csrc/hip -o tools/fold_policy tools/fold_policy.hip
-//   tools/fold_policy [rounds = 11]
+//         -Impich-pip_amd/csrc/hip -o tools/archive/fold_policy tools/archive/fold_policy.hip
+//   tools/archive/fold_policy [rounds = 11]
 //
 // 8 x 128 MiB at the collective's staging stride (block + 4352 B), three operand
 // sets rotated (3.4 GiB: nothing survives in the 256 MB Infinity Cache), HIP

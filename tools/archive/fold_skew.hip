@@ -7,8 +7,8 @@
 // output right after the eighth slot (as bench.py's config5_combine lays it).
 //
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off \
-//         -Impich-pip_amd/csrc/hip -o tools/fold_skew tools/fold_skew.hip
-//   tools/fold_skew [rounds = 9]
+//         -Impich-pip_amd/csrc/hip -o tools/archive/fold_skew tools/archive/fold_skew.hip
+//   tools/archive/fold_skew [rounds = 9]
 //
 // CHAIN8 fp16 and TREE8 fp32 over 8 blocks of 32-256 MiB (configs 5 and 4 at
 // 8 ranks: 128 / 32 MiB), CHAIN4 / TREE4 at config 5 / 4's 4-rank sizes; sets

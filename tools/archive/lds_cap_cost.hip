@@ -2,8 +2,8 @@
 // other work on the GPU at the same time.
 //
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -Impich-pip_amd/csrc/hip \
-//         -o tools/lds_cap_cost tools/lds_cap_cost.hip -lrccl
-//   tools/lds_cap_cost
+//         -o tools/archive/lds_cap_cost tools/archive/lds_cap_cost.hip -lrccl
+//   tools/archive/lds_cap_cost
 //
 // The library launches the P = 8 fold (k_combine_multi<.., 8, .., 1, 1024>)
 // with an unused 96 KiB dynamic LDS reservation: one 1024-thread workgroup per

@@ -6,7 +6,7 @@ allocator put them.  If HBM channel selection gives two operands at a
 power-of-two distance the same channels at the same moment, the synchronous
 call slows down the way the multi-operand folds did at an unskewed stride.
 
-    python tools/pair_offset.py [calls = 200]
+    python tools/archive/pair_offset.py [calls = 200]
 
 fp32 SUM, 256 MiB per operand, the synchronous MPI_Reduce_local (direct
 dispatch); kernel time from the CP timestamps (MPIR_Hip_direct_profile), the

@@ -4,7 +4,7 @@ counters, from one rocprofv3 run of the bench's timed loop (round 5).
     rocprofv3 --pmc TCP_UTCL1_TRANSLATION_MISS_sum TCP_UTCL1_TRANSLATION_HIT_sum \
         --kernel-trace --output-format csv -d OUT -o run -- \
         python3 bench.py --no-extras --no-cpu-baseline --no-variants --steps 400 --warmup 8
-    python tools/pair_pmc.py OUT
+    python tools/archive/pair_pmc.py OUT
 
 The bench rotates NPAIRS = 4 resident pairs, call i on pair i % 4, so the
 headline kernel's dispatches, in order, cycle over the pairs (the roofline

@@ -1,6 +1,6 @@
 """Are the headline loop's slow calls periodic in time?  (round 5)
 
-    python tools/slow_period.py [calls = 8000] [reps = 3]
+    python tools/archive/slow_period.py [calls = 8000] [reps = 3]
 
 The bench's synchronous 256 MiB fp32 SUM call, four resident pairs rotated, K
 calls back to back from C with a CLOCK_MONOTONIC stamp after each

@@ -1,5 +1,5 @@
 #!/bin/bash
-# One GPU-box call of round 5's measurements: the steps named on the command
+# One GPU-box call of a round's measurements (rounds 5-6): the steps named on the command
 # line, in order, each under its own time limit, stopping at the first failure.
 #   bash tools/gpu_round.sh TAG step...
 # steps:
@@ -11,9 +11,14 @@
 #   smoke      __graft_entry__.smoke()
 #   bench      python bench.py (defaults)
 #   prof       tools/profile_r03.sh: kernel trace + stats at 256 / 64 MiB, FETCH_SIZE and WRITE_SIZE passes
-#   lds        tools/lds_cap_cost (a fused fold beside a streaming kernel)
+#   lds        tools/archive/lds_cap_cost (a fused fold beside a streaming kernel)
 #   hostlat    tools/host_small_latency gpu
 #   driver6    python bench.py --steps 20 --warmup 5 (the driver's shape), six fresh processes
+#   bench20    python bench.py --steps 20 --warmup 5, once (round 6: one bench pass per product change)
+#   classifyt  tests/test_classify_kinds_gpu.py (pointer kinds, kept verdicts)
+#   place      tools/placement_ab.py (near / far / as-launched caller, alternated processes)
+#   place2     the same with the waiting knobs (lazy / delay / flush polls) beside near and far
+#   rotate     tools/fold_rotate (P = 8 fold with rotated operand reads)
 # Build every binary on the CPU side first (make -C mpich-pip_amd; hipcc lines
 # in each tool's header).
 set -o pipefail
@@ -39,7 +44,7 @@ for step in "$@"; do
            tail -5 $OUT/smoke.log ;;
     bench) timeout -k 10 400 python -u bench.py > $OUT/bench.log 2>&1; rc=$?; tail -c 3000 $OUT/bench.log ;;
     prof) timeout -k 10 1100 bash tools/profile_r03.sh $TAG > $OUT/prof.log 2>&1; rc=$?; tail -3 $OUT/prof.log ;;
-    lds) timeout -k 10 300 tools/lds_cap_cost > $OUT/lds_cap_cost.log 2>&1; rc=$?; cat $OUT/lds_cap_cost.log ;;
+    lds) timeout -k 10 300 tools/archive/lds_cap_cost > $OUT/lds_cap_cost.log 2>&1; rc=$?; cat $OUT/lds_cap_cost.log ;;
     hostlat) timeout -k 10 200 tools/host_small_latency gpu > $OUT/host_small_latency.log 2>&1; rc=$?
              cat $OUT/host_small_latency.log ;;
     driver6) rc=0
@@ -53,6 +58,15 @@ print(f"{sys.argv[1]}: value {d['value']} = {d['per_gpu']['frac_of_hbm_peak']}, 
       f"({d['roofline']['frac']}), call median {c['median_us']} p90 {c['p90_us']}, fixed {c['decomposition']['fixed_us']}")
 PY
              done ;;
+    bench20) timeout -k 10 400 python -u bench.py --steps 20 --warmup 5 > $OUT/bench20.log 2>&1; rc=$?
+             tail -c 3000 $OUT/bench20.log ;;
+    classifyt) timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread \
+                tests/test_classify_kinds_gpu.py > $OUT/pytest_classify.log 2>&1; rc=$?; tail -4 $OUT/pytest_classify.log ;;
+    place) timeout -k 10 600 python -u tools/placement_ab.py 4 2000 > $OUT/placement_ab.log 2>&1; rc=$?
+           tail -8 $OUT/placement_ab.log ;;
+    place2) timeout -k 10 900 python -u tools/placement_ab.py 3 2000 near,far,near:lazy,far:lazy,near:flush,near:delay \
+                > $OUT/placement_ab2.log 2>&1; rc=$?; tail -9 $OUT/placement_ab2.log ;;
+    rotate) timeout -k 10 400 tools/fold_rotate 9 > $OUT/fold_rotate.log 2>&1; rc=$?; cat $OUT/fold_rotate.log ;;
     *) echo "unknown step $step"; rc=2 ;;
     esac
     if [ $rc -ne 0 ]; then echo "step $step failed: $rc"; exit $rc; fi
