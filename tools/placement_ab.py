@@ -164,6 +164,11 @@ def child(mode: str, k: int) -> None:
 def main():
     if len(sys.argv) > 1 and sys.argv[1] == "--child":
         return child(sys.argv[2], int(sys.argv[3]))
+    if len(sys.argv) > 2 and sys.argv[1] == "--summarize":
+        # python3 tools/placement_ab.py --summarize LOG: the table again from a log's JSON lines
+        res = [json.loads(ln) for ln in open(sys.argv[2]) if ln.startswith("{")]
+        modes = list(dict.fromkeys(d["mode"] for d in res))
+        return summarize(res, modes)
     rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 4
     k = int(sys.argv[2]) if len(sys.argv) > 2 else 2000
     modes = sys.argv[3].split(",") if len(sys.argv) > 3 else ["near", "far", "none"]
@@ -185,6 +190,10 @@ def main():
             d["wall_s"] = round(time.time() - t0, 1)
             print(json.dumps(d), flush=True)
             res.append(d)
+    summarize(res, modes)
+
+
+def summarize(res, modes):
     print("\nmode        | loop median / mean us | window20 mean us | host->db | db->start | kernel | end->seen "
           "| 4 KiB call median: db->start, kernel, end->seen | cpu node / gpu / signal / errword")
     for mode in modes:
@@ -193,19 +202,19 @@ def main():
             print(f"{mode:11s} | skipped")
             continue
 
-        def mm(f):
-            v = sorted(f(d) for d in rs)
+        def mm(f, among=None):
+            v = sorted(f(d) for d in (among if among is not None else rs))
             return v[len(v) // 2]
         sp = [d for d in rs if d.get("split")]
         pl = rs[0]["placement"]
-        ss = [d for d in rs if d["small_4KiB"]["split"]]
+        ss = [d for d in rs if (d.get("small_4KiB") or {}).get("split")]
         print(f"{mode:11s} | {mm(lambda d: d['loop']['median_us']):7.2f} / {mm(lambda d: d['loop']['mean_us']):7.2f} | "
               f"{mm(lambda d: d['window20']['mean_us']):7.2f} | "
               + (" | ".join(f"{mm(lambda d, key=key: d['split'][key]):6.3f}" for key in
                             ("host_to_doorbell_us", "doorbell_to_start_us", "kernel_us", "end_to_seen_us"))
                  if sp else "-") +
-              f" | {mm(lambda d: d['small_4KiB']['loop']['median_us']):6.2f}: "
-              + (", ".join(f"{mm(lambda d, key=key: d['small_4KiB']['split'][key]):5.2f}" for key in
+              (f" | {mm(lambda d: d['small_4KiB']['loop']['median_us'], ss):6.2f}: " if ss else " | ")
+              + (", ".join(f"{mm(lambda d, key=key: d['small_4KiB']['split'][key], ss):5.2f}" for key in
                            ("doorbell_to_start_us", "kernel_us", "end_to_seen_us")) if ss else "-") +
               f" | {pl['cpu_node']} / {pl['gpu_node']} / {pl['signal_node']} / {pl['error_word_node']}")
 
