@@ -569,8 +569,19 @@ def bind_near_gpu(m, dev: int) -> dict:
     want = node_cpus(gnode) & allowed if gnode >= 0 else set()
     if not want:
         return {"mode": "unbound", "reason": f"no allowed CPU on the GPU's node ({gnode})", "gpu_node": gnode}
+    _LAUNCH_AFFINITY[:] = sorted(allowed)
     os.sched_setaffinity(0, want)          # this thread (and the threads it starts later)
     return {"mode": "gpu-node", "gpu_node": gnode, "cpus": len(want), "of_allowed": len(allowed)}
+
+
+_LAUNCH_AFFINITY: list = []
+
+
+def unbind() -> None:
+    """Back to the CPUs the process was launched with (the CPU baseline deals
+    its threads over every socket the job may use)."""
+    if _LAUNCH_AFFINITY:
+        os.sched_setaffinity(0, _LAUNCH_AFFINITY)
 
 
 def library_hip_runtime(lib):
@@ -1341,6 +1352,7 @@ def main():
 
     # the CPU baseline on rank 0 at every N, after the GPU work, the other
     # ranks parked on a blocking store read (no spinning core beside it)
+    unbind()
     if rank == 0 and not args.no_cpu_baseline:
         try:
             out["cpu_baseline"] = cpu_baseline(args, count, alg_bytes)

@@ -81,6 +81,14 @@ int MPIR_Hip_reduce(const void *inbuf, void *inoutbuf, uint64_t count, int op, i
 int MPIR_Hip_combine(const void *const *inbufs, int n, void *outbuf, uint64_t count, int op, int elem,
                      int order, void *hip_stream, int sync);
 
+/* Flags for the calling thread's later MPIR_Hip_combine calls; returns the
+ * previous flags.  MPIR_HIP_COMBINE_UNCAPPED: the fused folds run without the
+ * LDS reservation that caps a CU at one (P >= 5) or three (P = 3, 4) of their
+ * workgroups -- for a fold that overlaps other work on the device (the
+ * collectives' pipelined folds beside RCCL's transfers). */
+#define MPIR_HIP_COMBINE_UNCAPPED 1
+int MPIR_Hip_combine_set_flags(int flags);
+
 /* byte size of an element class (0 if unknown) */
 size_t MPIR_Hip_elem_size(int elem);
 /* 1 if a kernel exists for (op, elem) */

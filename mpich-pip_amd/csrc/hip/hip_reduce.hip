@@ -65,6 +65,10 @@ std::atomic<uint64_t> g_keep{[] {
 uint64_t keep_bytes() { return g_keep.load(std::memory_order_relaxed); }
 
 uint64_t keep_for(uint64_t vbytes) { return vbytes <= keep_bytes() ? vbytes : 0; }
+
+// MPIR_Hip_combine_set_flags: the calling thread's combine flags
+thread_local int t_combine_flags = 0;
+bool multi_uncapped() { return (t_combine_flags & MPIR_HIP_COMBINE_UNCAPPED) != 0; }
 }  // namespace mpir_hip
 
 namespace {
@@ -1101,6 +1105,12 @@ int MPIR_Hip_set_local_ranks(int n) {
 }
 
 int MPIR_Hip_host_threads(void) { return pool_threads(); }
+
+int MPIR_Hip_combine_set_flags(int flags) {
+    const int prev = mpir_hip::t_combine_flags;
+    mpir_hip::t_combine_flags = flags & MPIR_HIP_COMBINE_UNCAPPED;
+    return prev;
+}
 
 int MPIR_Hip_thread_contexts(void) {
     std::lock_guard<std::mutex> lk(g_pool_mu);

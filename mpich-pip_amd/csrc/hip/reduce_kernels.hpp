@@ -751,6 +751,12 @@ constexpr int multi_cap_bytes() {
            : (P >= 5 && TH == 1024) ? (96 << 10)
            : ((P == 4 || P == 3) && TH == kThreads) ? (53 << 10) : 0;
 }
+// Per call (MPIR_Hip_combine_set_flags, MPIR_HIP_COMBINE_UNCAPPED): a fold
+// that runs beside other kernels -- the device collectives' pipelined fold,
+// overlapping RCCL's transfer kernels -- goes without the reservation, which
+// would hold every CU to one of its workgroups and slow the kernels beside it
+// (tools/archive/lds_cap_cost.hip).
+bool multi_uncapped();      // the calling thread's flag (hip_reduce.hip)
 template <class Op, class T, int P, bool TREE, int U, int TH>
 size_t multi_lds_cap() {
     constexpr int cap = multi_cap_bytes<P, TH>();
@@ -791,7 +797,7 @@ hipError_t launch_combine_pu(const void *const *ins, void *out_, uint64_t count,
         a.tail_off = (int64_t)vbytes;
         uint64_t grid = (vbytes + tile - 1) / tile;
         if (grid == 0) grid = 1;
-        const size_t lds = multi_lds_cap<Op, T, P, TREE, U, TH>();
+        const size_t lds = multi_uncapped() ? 0 : multi_lds_cap<Op, T, P, TREE, U, TH>();
         hipLaunchKernelGGL((k_combine_multi<Op, T, P, TREE, U, TH>), dim3((unsigned)grid), dim3(TH), lds, s, a);
     } else {
         a.out = out;

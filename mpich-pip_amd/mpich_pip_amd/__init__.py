@@ -121,7 +121,7 @@ EXPORTED_SYMBOLS = [
     "MPIR_Hip_pointer_kind", "MPIR_Hip_memcpy", "MPIR_Hip_error_string", "MPIR_Hip_device_count", "MPIR_Hip_thread_contexts",
     "MPIR_Hip_host_max_bytes", "MPIR_Hip_set_host_max_bytes", "MPIR_Hip_mixed_max_bytes", "MPIR_Hip_direct_dispatches", "MPIR_Hip_direct_profile",
     "MPIR_Hip_direct_last_kernel_ns", "MPIR_Hip_direct_state", "MPIR_Hip_direct_busy_skips",
-    "MPIR_Hip_direct_last_split", "MPIR_Hip_direct_kernarg_writes", "MPIR_Hip_direct_placement", "MPIR_Hip_build_id",
+    "MPIR_Hip_direct_last_split", "MPIR_Hip_direct_kernarg_writes", "MPIR_Hip_direct_placement", "MPIR_Hip_build_id", "MPIR_Hip_combine_set_flags",
     "MPIR_Hip_direct_prepare", "MPIR_Hip_set_local_ranks", "MPIR_Hip_host_threads",
     # runtime subset for config 1 (include/mpi_pip.h)
     "MPI_Init", "MPI_Initialized", "MPI_Finalize", "MPI_Finalized", "MPI_Abort", "MPI_Comm_size",
@@ -213,6 +213,8 @@ def load(path: str | None = None) -> ctypes.CDLL:
     lib.MPIR_Hip_host_threads.argtypes = []
     lib.MPIR_Hip_host_threads.restype = i32
     lib.MPIR_Hip_build_id.restype = ctypes.c_char_p
+    lib.MPIR_Hip_combine_set_flags.argtypes = [i32]
+    lib.MPIR_Hip_combine_set_flags.restype = i32
     lib.MPIR_Hip_error_string.restype = ctypes.c_char_p
     lib.MPIR_Hip_pointer_kind.argtypes = [vp, ctypes.c_uint64]
     lib.MPIR_Hip_pointer_kind.restype = i32

@@ -91,6 +91,13 @@ size_t MPIR_Hip_elem_size(int elem) { return elem > 0 && elem < MPIR_HIP_NELEMS 
 int MPIR_Hip_has_kernel(int op, int elem) { (void) op; return elem > 0 && elem < MPIR_HIP_NELEMS; }
 const char *MPIR_Hip_error_string(void) { return ""; }
 int MPIR_Hip_is_device_ptr(const void *p) { (void) p; return 1; }
+int MPIR_Hip_combine_set_flags(int flags)
+{
+    static int cur;
+    const int prev = cur;
+    cur = flags;
+    return prev;
+}
 int MPIR_Hip_memcpy(void *d, const void *s, size_t n) { (void) d; (void) s; (void) n; return MPIR_HIP_OK; }
 int MPIR_Hip_reduce(const void *in, void *io, uint64_t count, int op, int elem, void *s, int sync)
 {

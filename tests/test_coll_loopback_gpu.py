@@ -448,3 +448,60 @@ def test_large_blocks_skewed_staging(mpi, orc, cuda, p):
     finally:
         for c in comms:
             mpi.comm_free(c)
+
+
+PIPE = [("MPI_FLOAT", "MPI_SUM"), ("MPIX_C_FLOAT16", "MPI_SUM"), ("MPI_DOUBLE", "MPI_MAX"), ("MPI_INT", "MPI_BXOR")]
+
+
+@pytest.mark.parametrize("t,op", PIPE, ids=[f"{t}-{o}" for t, o in PIPE])
+@pytest.mark.parametrize("p", [2, 3, 5, 8])
+@pytest.mark.parametrize("kind", ["allreduce", "reduce_scatter_block", "reduce"])
+def test_pipelined_reference_order(mpi, orc, cuda, t, op, p, kind, monkeypatch):
+    """The reference-order schedules with the exchange cut into chunks and each
+    chunk's fold overlapping the next chunk's transfer (coll_hip.c
+    exchange_fold_pipelined; MPIR_CVAR_DEVICE_COLL_PIPELINE_KB = 64 here so
+    that test-sized blocks span many chunks, ragged last chunks included):
+    bit-exact against the oracle's step-by-step schedules, every rank."""
+    from oracle import schedules as S
+    monkeypatch.setenv("MPIR_CVAR_DEVICE_COLL_PIPELINE_KB", "64")
+    torch = cuda
+    esz = T.elem_size(t)
+    comms = mpi.comm_create_loopback(p)
+    try:
+        count = (1 << 19) + 7 if kind != "reduce_scatter_block" else (1 << 17) + 5
+        rng = np.random.default_rng(17 * p + len(kind))
+        n = count * p if kind == "reduce_scatter_block" else count
+        xs = [T.to_bytes(T.gen(t, n, rng, op)) for _ in range(p)]
+        root = p - 1
+        if kind == "allreduce":
+            want = [S.allreduce_smp_auto(xs, count, esz, mpi.DATATYPES[t], mpi.OPS[op])] * p
+        elif kind == "reduce_scatter_block":
+            want = S.reduce_scatter_block_auto(xs, count, esz, mpi.DATATYPES[t], mpi.OPS[op])
+        else:
+            want = {root: S.reduce_auto(xs, count, esz, mpi.DATATYPES[t], mpi.OPS[op], root)}
+        send = [torch.from_numpy(x.copy()).cuda() for x in xs]
+        recv = [torch.zeros(count * esz, dtype=torch.uint8, device="cuda") for _ in range(p)]
+        torch.cuda.synchronize()
+
+        def rank(r):
+            if kind == "allreduce":
+                rc = mpi.allreduce(send[r].data_ptr(), recv[r].data_ptr(), count, mpi.DATATYPES[t], mpi.OPS[op],
+                                   comms[r], mpi.MPIX_HIP_ALG_REFERENCE_ORDER)
+            elif kind == "reduce_scatter_block":
+                rc = mpi.reduce_scatter_block(send[r].data_ptr(), recv[r].data_ptr(), count, mpi.DATATYPES[t],
+                                              mpi.OPS[op], comms[r], mpi.MPIX_HIP_ALG_REFERENCE_ORDER)
+            else:
+                rc = mpi.reduce(send[r].data_ptr(), recv[r].data_ptr() if r == root else 0, count,
+                                mpi.DATATYPES[t], mpi.OPS[op], root, comms[r], mpi.MPIX_HIP_ALG_REFERENCE_ORDER)
+            assert rc == 0, mpi.error_string(rc)
+
+        run_ranks(rank, p)
+        torch.cuda.synchronize()
+        for r in range(p):
+            if kind == "reduce" and r != root:
+                continue
+            got = recv[r].cpu().numpy()
+            assert same(got, want[r], t), f"rank {r}: {np.count_nonzero(got != want[r])} bytes differ"
+    finally:
+        for c in comms:
+            mpi.comm_free(c)

@@ -223,3 +223,40 @@ def test_checker_catches_changed_sequences(harness):
         j = next(j for j, e in enumerate(logs[1]) if e[0] == "group_start")
         logs[1].insert(j + 1, ev)
     mutated(inside)
+
+
+@pytest.mark.parametrize("kb,chunks", [(0, 1), (32768, 4), (65536, 2)])
+def test_pipelined_reference_order_chunks(harness, kb, chunks, monkeypatch):
+    """Config 5's reference order at N = 8 (8 x 128 MiB blocks): with
+    MPIR_CVAR_DEVICE_COLL_PIPELINE_KB = chunk, the exchange runs in
+    128 MiB / chunk groups and the CHAIN8 fold in as many chunk folds, each
+    chunk's fold after its group (coll_hip.c exchange_fold_pipelined); 0 turns
+    the pipeline off.  The cross-rank rules hold either way."""
+    monkeypatch.setenv("MPIR_CVAR_DEVICE_COLL_PIPELINE_KB", str(kb))
+    n = 8
+    logs = run_plan(harness, n, [config5(n)[1]], f"pipe{kb}")
+    res = check(logs)
+    for r, log in enumerate(logs):
+        assert res[r]["groups"] == chunks
+        folds = [ev for ev in log if ev[:2] == ["note", "combine"]]
+        assert len(folds) == chunks
+        assert sum(int(ev[3]) for ev in folds) == (1 << 29) // n          # every element folded once
+        assert all(ev[2] == "8" and ev[-1] == "chain" for ev in folds)
+        # each fold follows its chunk's group
+        pos = [i for i, ev in enumerate(log) if ev[0] == "group_end"]
+        fpos = [i for i, ev in enumerate(log) if ev[:2] == ["note", "combine"]]
+        assert all(f > g for f, g in zip(fpos, pos))
+
+
+@pytest.mark.parametrize("n", [3, 5, 6, 7])
+def test_pipelined_allreduce_non_pof2(harness, n):
+    """Config 4's reference order at rank counts with a pre-fold (excluded
+    ranks take part in every chunk's group with no transfers): the blocks of
+    256 MiB / pof2 are pipelined, and the sequences still match."""
+    logs = run_plan(harness, n, [CONFIG4[1]], "arnp")
+    res = check(logs)
+    pof2 = 1 << (n.bit_length() - 1)
+    block = (256 << 20) // pof2
+    chunks = -(-block // (32 << 20))
+    # pre-fold group + reduce-scatter chunks + allgather chunks
+    assert all(pr["groups"] == 1 + 2 * chunks for pr in res), [pr["groups"] for pr in res]

@@ -34,6 +34,7 @@
 namespace mpir_hip {
 uint64_t keep_bytes() { return kKeepBytes; }
 uint64_t keep_for(uint64_t vbytes) { return vbytes <= keep_bytes() ? vbytes : 0; }
+bool multi_uncapped() { return false; }
 }
 using namespace mpir_hip;
 

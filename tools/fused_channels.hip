@@ -35,6 +35,7 @@
 namespace mpir_hip {
 static uint64_t g_keep = 0;
 uint64_t keep_for(uint64_t vbytes) { return vbytes <= g_keep ? vbytes : 0; }
+bool multi_uncapped() { return false; }
 }  // namespace mpir_hip
 
 using namespace mpir_hip;

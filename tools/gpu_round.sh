@@ -18,6 +18,9 @@
 #   classifyt  tests/test_classify_kinds_gpu.py (pointer kinds, kept verdicts)
 #   place      tools/placement_ab.py (near / far / as-launched caller, alternated processes)
 #   place2     the same with the waiting knobs (lazy / delay / flush polls) beside near and far
+#   pipe       the collectives' GPU tests (loopback, config sizes, fused schedules)
+#   overlap    tools/pipeline_overlap (fold beside a one-rank RCCL transfer, serial vs overlapped, capped or not)
+#   pipeab     tools/pipeline_ab.py (config 5 through the loopback, pipelined vs not)
 #   rotate     tools/fold_rotate (P = 8 fold with rotated operand reads)
 # Build every binary on the CPU side first (make -C mpich-pip_amd; hipcc lines
 # in each tool's header).
@@ -66,6 +69,13 @@ PY
            tail -8 $OUT/placement_ab.log ;;
     place2) timeout -k 10 900 python -u tools/placement_ab.py 3 2000 near,far,near:lazy,far:lazy,near:flush,near:delay \
                 > $OUT/placement_ab2.log 2>&1; rc=$?; tail -9 $OUT/placement_ab2.log ;;
+    pipe) timeout -k 10 400 python -u -m pytest -x -q --timeout 200 --timeout-method thread \
+                tests/test_coll_loopback_gpu.py tests/test_config_size_gpu.py tests/test_schedule_fused_gpu.py \
+                > $OUT/pytest_pipe.log 2>&1; rc=$?; tail -2 $OUT/pytest_pipe.log ;;
+    overlap) timeout -k 10 200 tools/pipeline_overlap 15 > $OUT/pipeline_overlap.log 2>&1; rc=$?
+             cat $OUT/pipeline_overlap.log ;;
+    pipeab) timeout -k 10 300 python -u tools/pipeline_ab.py 7 > $OUT/pipeline_ab.log 2>&1; rc=$?
+            cat $OUT/pipeline_ab.log ;;
     rotate) timeout -k 10 400 tools/fold_rotate 9 > $OUT/fold_rotate.log 2>&1; rc=$?; cat $OUT/fold_rotate.log ;;
     *) echo "unknown step $step"; rc=2 ;;
     esac

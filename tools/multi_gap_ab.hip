@@ -22,6 +22,7 @@
 namespace mpir_hip {
 uint64_t keep_bytes() { return getenv("KEEP_MB") ? strtoull(getenv("KEEP_MB"), 0, 10) << 20 : kKeepBytes; }
 uint64_t keep_for(uint64_t vbytes) { return vbytes <= keep_bytes() ? vbytes : 0; }
+bool multi_uncapped() { return false; }
 }
 using namespace mpir_hip;
 
