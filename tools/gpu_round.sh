@@ -21,6 +21,7 @@
 #   pipe       the collectives' GPU tests (loopback, config sizes, fused schedules)
 #   overlap    tools/pipeline_overlap (fold beside a one-rank RCCL transfer, serial vs overlapped, capped or not)
 #   pipeab     tools/pipeline_ab.py (config 5 through the loopback, pipelined vs not)
+#   overhead   tools/timing_overhead.py (the timed region's bracketing cost; raw profiled splits), near and unbound
 #   rotate     tools/fold_rotate (P = 8 fold with rotated operand reads)
 # Build every binary on the CPU side first (make -C mpich-pip_amd; hipcc lines
 # in each tool's header).
@@ -76,6 +77,9 @@ PY
              cat $OUT/pipeline_overlap.log ;;
     pipeab) timeout -k 10 300 python -u tools/pipeline_ab.py 7 > $OUT/pipeline_ab.log 2>&1; rc=$?
             cat $OUT/pipeline_ab.log ;;
+    overhead) { timeout -k 10 120 python3 -u tools/timing_overhead.py > $OUT/overhead_near.log 2>&1 &&
+                timeout -k 10 120 python3 -u tools/timing_overhead.py unbound > $OUT/overhead_none.log 2>&1; }; rc=$?
+              cat $OUT/overhead_near.log $OUT/overhead_none.log ;;
     rotate) timeout -k 10 400 tools/fold_rotate 9 > $OUT/fold_rotate.log 2>&1; rc=$?; cat $OUT/fold_rotate.log ;;
     *) echo "unknown step $step"; rc=2 ;;
     esac
