@@ -263,7 +263,7 @@ def run_collectives_child(rank: int, world: int, local: int, barrier, timeout: f
 
 
 def time_loop(run, k: int, w: int, sync, barrier, max_over_ranks, own: list | None = None,
-              calls: list | None = None, gap: list | None = None) -> float:
+              calls: list | None = None, gap: list | None = None, bracket: list | None = None) -> float:
     """time_steps for a C loop: run(start, n[, stamps]) makes steps start ..
     start + n - 1 back to back; W untimed steps, then exactly K timed ones
     between barrier + device sync, max over ranks.  `calls`, if given, receives
@@ -291,6 +291,10 @@ def time_loop(run, k: int, w: int, sync, barrier, max_over_ranks, own: list | No
     if calls is not None:
         import numpy as np
         stamps = np.zeros(k + 1, np.int64)
+    # Python's cyclic collector held off while the K calls run, as in
+    # time_steps (and timeit)
+    gc_on = gc.isenabled()
+    gc.disable()
     t0 = time.perf_counter()
     if stamps is None:
         run(w, k)
@@ -298,7 +302,13 @@ def time_loop(run, k: int, w: int, sync, barrier, max_over_ranks, own: list | No
         run(w, k, stamps)
     sync()
     t1 = time.perf_counter()
+    if gc_on:
+        gc.enable()
     barrier()
+    if bracket is not None and stamps is not None:
+        # the timed region around the K calls: the Python -> C loop entry and
+        # exit and the closing torch.cuda.synchronize() (same clock)
+        bracket.append((t1 - t0) - (int(stamps[k]) - int(stamps[0])) * 1e-9)
     if own is not None:
         own.append(t1 - t0)
     if calls is not None:
@@ -352,7 +362,8 @@ def park_until_rank0(use_pg: bool, world: int, rank: int, dist, key: str, timeou
 
 
 def sync_loops(m, lib, reduce_local, ptrs, count, k: int, w: int, sync, barrier, max_over_ranks,
-               own: list | None = None, c_loop=None, calls: list | None = None, gap: list | None = None):
+               own: list | None = None, c_loop=None, calls: list | None = None, gap: list | None = None,
+               bracket: list | None = None):
     """The headline loop (NPAIRS pairs rotated: every call after the first
     NPAIRS repeats its kernel arguments, which the direct dispatch's kernarg
     cache then holds) and the same loop with fresh arguments on every call: the
@@ -387,7 +398,7 @@ def sync_loops(m, lib, reduce_local, ptrs, count, k: int, w: int, sync, barrier,
         return run
     dt_py = None
     if c_loop is not None:
-        dt = time_loop(runner(call_args), k, w, sync, barrier, max_over_ranks, own, calls, gap)
+        dt = time_loop(runner(call_args), k, w, sync, barrier, max_over_ranks, own, calls, gap, bracket)
         kw0 = lib.MPIR_Hip_direct_kernarg_writes()
         dtf = time_loop(runner(fresh_args), k, w, sync, barrier, max_over_ranks, own)
         writes = (lib.MPIR_Hip_direct_kernarg_writes() - kw0) / (k + w)
@@ -492,7 +503,7 @@ def direct_kernel_ns(lib, call, k: int, w: int, splits: list | None = None):
             ns.append(lib.MPIR_Hip_direct_last_kernel_ns())
             if splits is not None:
                 lib.MPIR_Hip_direct_last_split(sp)
-                splits.append(tuple(sp))
+                splits.append(tuple(v - (1 << 64) if v >= (1 << 63) else v for v in sp))     # (signed ns)
         if lib.MPIR_Hip_direct_dispatches() - before != k or min(ns) <= 0:
             return None
         return ns
@@ -505,7 +516,12 @@ def split_medians(splits: list) -> dict | None:
     timelines (direct_kernel_ns): entry -> doorbell (host), doorbell -> CP
     dispatch start, the kernel (CP start -> end), CP end -> host sees the
     completion signal.  The profiled calls run on the timestamped twin queue."""
-    rows = [s for s in splits if 0 < s[0] <= s[1] <= s[2] <= s[3]]
+    # (the CP's timestamps reach the host clock through the runtime's clock
+    # translation, whose offset can be a few us: the split keeps the intervals
+    # that do not depend on it -- entry -> doorbell (host clock), the kernel (CP
+    # clock), doorbell -> host sees completion minus the kernel -- and reports
+    # doorbell -> dispatch start as translated)
+    rows = [s for s in splits if 0 < s[0] < s[3] and 0 < s[2] - s[1] < s[3] - s[0]]
     if not rows:
         return None
 
@@ -514,9 +530,9 @@ def split_medians(splits: list) -> dict | None:
         return round(v[len(v) // 2] * 1e-3, 2)
     return {"calls": len(rows),
             "host_to_doorbell_us": med([s[0] for s in rows]),
-            "doorbell_to_dispatch_start_us": med([s[1] - s[0] for s in rows]),
             "kernel_us": med([s[2] - s[1] for s in rows]),
-            "end_to_host_seen_us": med([s[3] - s[2] for s in rows]),
+            "doorbell_to_seen_minus_kernel_us": med([(s[3] - s[0]) - (s[2] - s[1]) for s in rows]),
+            "doorbell_to_dispatch_start_us_translated": med([s[1] - s[0] for s in rows]),
             "source": "MPIR_Hip_direct_last_split over the K profiled calls (timestamped twin queue; host clock "
                       "stamps around the CP's dispatch timestamps)"}
 
@@ -1080,12 +1096,12 @@ def main():
         binding = "C loop of the compiled binding (csrc/py/fastcall.c reduce_local_loop)"
     except ImportError:     # extension not built: the same C entry point through ctypes
         reduce_local, c_loop, binding = lib.MPI_Reduce_local, None, "ctypes"
-    own, calls, gap = [], [], []
+    own, calls, gap, bracket = [], [], [], []
     place_before = m.placement(dev)
     d_before = lib.MPIR_Hip_direct_dispatches()
     dt, dt_fresh, fresh_writes, step, dt_py = sync_loops(m, lib, reduce_local, ptrs, count, args.steps,
                                                          args.warmup, sync, barrier, max_over_ranks, own, c_loop,
-                                                         calls, gap)
+                                                         calls, gap, bracket)
     # timed call i is step W + i: operand pair (W + i) % NPAIRS
     cstats = call_stats(calls, alg_bytes, [(args.warmup + i) % NPAIRS for i in range(len(calls))])
     if calls:
@@ -1095,6 +1111,8 @@ def main():
         cstats["first_call_us"] = round(calls[0] * 1e6, 2)
         if gap:
             cstats["idle_gap_before_first_us"] = round(gap[0] * 1e6, 1)
+        if bracket:
+            cstats["timed_region_outside_calls_us"] = round(bracket[0] * 1e6, 2)
     direct_share = (lib.MPIR_Hip_direct_dispatches() - d_before) / ((3 if c_loop else 2) * (args.steps + args.warmup))
     value = alg_bytes * args.steps * world / dt / GIB
     # each rank's own figures beside the max-over-ranks `value`: a lagging GPU,

@@ -160,7 +160,9 @@ int MPIR_Hip_direct_state(int dev);
 int MPIR_Hip_direct_prepare(int dev);
 /* With profiling on, the calling thread's last direct call on the system
  * clock, ns from entering the dispatch: doorbell rung, CP start, CP end,
- * completion seen by the host. */
+ * completion seen by the host.  The CP's two stamps reach the system clock
+ * through the runtime's translation, so they carry its offset (a few us at
+ * most) and are two's-complement int64 values in the uint64 slots. */
 void MPIR_Hip_direct_last_split(uint64_t out[4]);
 uint64_t MPIR_Hip_direct_busy_skips(void);
 /* Direct calls whose kernel arguments missed the kernarg cache (written into a

@@ -955,8 +955,10 @@ int direct_reduce(int dev, int op, int elem, const ReducePlan &p, int *rc) {
         t_last_kernel_ns = okt ? (uint64_t)((double)(t.end - t.start) * ns) : 0;
         // the dispatch times are in the system domain, like HSA_SYSTEM_INFO_TIMESTAMP
         t_last_split[0] = (uint64_t)((double)(th1 - th0) * ns);
-        t_last_split[1] = okt ? (uint64_t)((double)((int64_t)(t.start - th0)) * ns) : 0;
-        t_last_split[2] = okt ? (uint64_t)((double)((int64_t)(t.end - th0)) * ns) : 0;
+        // (the CP's stamps come through the runtime's clock translation: one
+        // may land before th0 -- stored as a two's-complement int64)
+        t_last_split[1] = okt ? (uint64_t)(int64_t)((double)((int64_t)(t.start - th0)) * ns) : 0;
+        t_last_split[2] = okt ? (uint64_t)(int64_t)((double)((int64_t)(t.end - th0)) * ns) : 0;
         t_last_split[3] = (uint64_t)((double)(th2 - th0) * ns);
     }
     g_direct_calls.fetch_add(1, std::memory_order_relaxed);

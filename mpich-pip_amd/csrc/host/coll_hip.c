@@ -378,9 +378,11 @@ static int group_exchange(struct MPIX_Hip_comm_s *c, const xfer_t *sends, int ns
  * runs on the communicator's fold stream while chunk k+1 moves: the folds
  * hide behind the transfers.  Element-wise folds over the same operands in the
  * same order: the results are bit-identical to the unchunked schedule.  The
- * pipelined folds run without their LDS cap (MPIR_HIP_COMBINE_UNCAPPED): the
- * cap holds every CU to one fold workgroup, which slowed a one-rank RCCL
- * all_reduce beside it 2.6x.
+ * pipelined folds keep their LDS cap: beside RCCL's kernel the capped fold
+ * leaves it faster than the uncapped one (a one-rank all_reduce 56.9 against
+ * 71.2 us, 21.8 alone), and in the pipeline the two are within
+ * 1 % (tools/pipeline_overlap.cpp, profiles/r06/pipeline_overlap.log); a caller
+ * that wants the other choice has MPIR_Hip_combine_set_flags.
  * MPIR_CVAR_DEVICE_COLL_PIPELINE_KB: the chunk (default 32768 = 32 MiB; 0 =
  * never pipeline); a schedule pipelines when its largest block spans at least
  * two chunks, in at most MAX_PIPE chunks. */
@@ -447,7 +449,7 @@ static int exchange_fold_pipelined(struct MPIX_Hip_comm_s *c, const xfer_t *send
                                    chunk_fold_fn fold, void *ctx)
 {
     xfer_t sk[MAX_XFER], rk[MAX_XFER];
-    int k, rc = MPI_SUCCESS, prev = MPIR_Hip_combine_set_flags(MPIR_HIP_COMBINE_UNCAPPED);
+    int k, rc = MPI_SUCCESS;
     hipError_t e = hipSuccess;
     for (k = 0; k < nchunk && rc == MPI_SUCCESS; k++) {
         size_t off = (size_t) k * chunk;
@@ -464,7 +466,6 @@ static int exchange_fold_pipelined(struct MPIX_Hip_comm_s *c, const xfer_t *send
         if ((e = hipEventRecord(c->fev[k], c->fold_stream)) != hipSuccess)
             break;
     }
-    (void) MPIR_Hip_combine_set_flags(prev);
     if (e != hipSuccess) {
         MPIR_Err_set_detail("pipelined schedule: %s", hipGetErrorString(e));
         return MPI_ERR_OTHER;

@@ -1,4 +1,4 @@
-"""The committed bench line (profiles/r05/bench_r05au.log, measured on MI355X) against
+"""The committed bench line (profiles/r06/bench_r06c.log, measured on MI355X) against
 the driver's contract and against itself: BASELINE.json's metric, the
 required keys, value = algorithmic bytes x N / time, roofline.frac =
 achieved / peak with achieved = 805,306,368 B / mean launch time, and the
@@ -10,7 +10,7 @@ import os
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LINE = os.path.join(ROOT, "profiles", "r05", "bench_r05au.log")
+LINE = os.path.join(ROOT, "profiles", "r06", "bench_r06c.log")
 GIB = float(1 << 30)
 
 
@@ -110,3 +110,28 @@ def test_call_distribution(line):
     assert cd["min_us"] <= cd["first_call_us"] <= cd["max_us"]
     assert 0.0 < cd["idle_gap_before_first_us"] < 50.0
     assert "after the barrier" in line["value_conditions"]["warmup"]
+
+
+def test_placement_recorded_and_bound(line):
+    """Round 6: every rank's placement -- its CPU and NUMA
+    node before and after the timed loop, its GPU's node, the nodes of the
+    completion signal and error word -- and the binding the bench applied: the
+    calling thread on its GPU's node (value_conditions.placement), with the
+    as-launched loop beside it (sync_variants.launch_placement)."""
+    for r in line["per_rank"]:
+        pl = r["placement"]
+        for k in ("cpu_before_loop", "cpu_after_loop", "cpu_node", "gpu_node", "signal_node", "error_word_node",
+                  "allowed_cpus"):
+            assert k in pl, k
+        assert pl["gpu_node"] >= 0 and pl["cpu_node"] == pl["gpu_node"]      # bound near its GPU
+    vc = line["value_conditions"]["placement"]
+    assert vc["mode"] == "gpu-node" and vc["gpu_node"] == line["per_rank"][0]["placement"]["gpu_node"]
+    lp = line["sync_variants"]["launch_placement"]
+    assert lp["value"] > 0 and lp["placement"]["gpu_node"] == vc["gpu_node"]
+    assert "BENCH_BIND=none" in lp["env"]
+
+
+def test_build_id_in_line(line):
+    """Round 6: the line names the sources its binaries came from."""
+    bid = dict(kv.split("=", 1) for kv in line["config"]["build_id"].split())
+    assert set(bid) == {"src", "tiles", "git"} and len(bid["src"]) == 16 and len(bid["tiles"]) == 16

@@ -118,10 +118,10 @@ def child(mode: str, k: int) -> None:
         for i in range(min(k, 400)):
             assert loop(sets, i, 1) == 0
             lib.MPIR_Hip_direct_last_split(sp)
-            rows.append(tuple(sp))
+            rows.append(tuple(v - (1 << 64) if v >= (1 << 63) else v for v in sp))
     finally:
         lib.MPIR_Hip_direct_profile(0)
-    rows = [r for r in rows if 0 < r[0] <= r[1] <= r[2] <= r[3]]
+    rows = [r for r in rows if 0 < r[0] < r[3] and 0 < r[2] - r[1] < r[3] - r[0]]
 
     def med(v):
         v = sorted(v)
@@ -144,10 +144,10 @@ def child(mode: str, k: int) -> None:
         for i in range(400):
             assert loop(sset, 0, 1) == 0
             lib.MPIR_Hip_direct_last_split(sp)
-            srows.append(tuple(sp))
+            srows.append(tuple(v - (1 << 64) if v >= (1 << 63) else v for v in sp))
     finally:
         lib.MPIR_Hip_direct_profile(0)
-    srows = [r for r in srows if 0 < r[0] <= r[1] <= r[2] <= r[3]]
+    srows = [r for r in srows if 0 < r[0] < r[3] and 0 < r[2] - r[1] < r[3] - r[0]]
     small_split = {"host_to_doorbell_us": med([r[0] for r in srows]),
                    "doorbell_to_start_us": med([r[1] - r[0] for r in srows]),
                    "kernel_us": med([r[2] - r[1] for r in srows]),
