@@ -725,6 +725,46 @@ int device_node(int dev) {
 }
 }  // namespace
 
+// MPIR_CVAR_REDUCE_LOCAL_BIND=gpu-node (opt-in, default off): at its first
+// direct call on a device, the calling thread binds itself to the CPUs of that
+// device's NUMA node (within the CPUs it may already use) -- for programs whose
+// launcher does not bind GPU ranks (Hydra binds nothing by default).  A caller
+// near its GPU saves ~2 us per synchronous call (DESIGN.md §(d), "Where the
+// caller runs").  A library changing its caller's affinity is a side effect, so
+// it is only done when asked.
+static void maybe_bind_near(int dev) {
+    static const bool on = [] {
+        const char *e = getenv("MPIR_CVAR_REDUCE_LOCAL_BIND");
+        return e && !strcmp(e, "gpu-node");
+    }();
+    thread_local bool done = false;
+    if (!on || done) return;
+    done = true;
+    const int node = device_node(dev);
+    if (node < 0) return;
+    char path[96];
+    snprintf(path, sizeof path, "/sys/devices/system/node/node%d/cpulist", node);
+    FILE *f = fopen(path, "r");
+    if (!f) return;
+    cpu_set_t want, have;
+    CPU_ZERO(&want);
+    char buf[4096];
+    if (fgets(buf, sizeof buf, f)) {
+        for (char *t = strtok(buf, ",\n"); t; t = strtok(nullptr, ",\n")) {
+            int a = -1, b = -1;
+            if (sscanf(t, "%d-%d", &a, &b) == 2) {
+                for (int c = a; c <= b && c < CPU_SETSIZE; ++c) CPU_SET(c, &want);
+            } else if (sscanf(t, "%d", &a) == 1 && a >= 0 && a < CPU_SETSIZE) {
+                CPU_SET(a, &want);
+            }
+        }
+    }
+    fclose(f);
+    if (pthread_getaffinity_np(pthread_self(), sizeof have, &have) != 0) return;
+    CPU_AND(&want, &want, &have);
+    if (CPU_COUNT(&want) > 0) (void)pthread_setaffinity_np(pthread_self(), sizeof want, &want);
+}
+
 // out: the calling thread's CPU, that CPU's NUMA node, device dev's NUMA node,
 // the node of the page holding this thread's completion signal for dev (-1
 // before its first direct call, or unknown), the node of the device's error
@@ -771,6 +811,7 @@ int direct_reduce(int dev, int op, int elem, const ReducePlan &p, int *rc) {
     if (mode() == 0 || dev < 0 || dev >= kMaxDirectDev || op <= 0 || op >= MPIR_HIP_NOPS || elem <= 0 ||
         elem >= MPIR_HIP_NELEMS || p.kind < 0 || p.kind >= kPlanKinds || p.arg_bytes != kPlanArgBytes[p.kind])
         return 0;
+    maybe_bind_near(dev);
     const bool prof = g_profile.load(std::memory_order_relaxed) != 0;
     const uint64_t th0 = prof ? sys_ts() : 0;
     uint64_t th1 = 0;

@@ -22,6 +22,7 @@
 #   overlap    tools/pipeline_overlap (fold beside a one-rank RCCL transfer, serial vs overlapped, capped or not)
 #   pipeab     tools/pipeline_ab.py (config 5 through the loopback, pipelined vs not)
 #   overhead   tools/timing_overhead.py (the timed region's bracketing cost; raw profiled splits), near and unbound
+#   share2     BENCH_TEST_SHARE_GPU=1 bench.py --gpus 2 (the N > 1 path rehearsed on one GPU; not a measurement)
 #   rotate     tools/fold_rotate (P = 8 fold with rotated operand reads)
 # Build every binary on the CPU side first (make -C mpich-pip_amd; hipcc lines
 # in each tool's header).
@@ -80,6 +81,8 @@ PY
     overhead) { timeout -k 10 120 python3 -u tools/timing_overhead.py > $OUT/overhead_near.log 2>&1 &&
                 timeout -k 10 120 python3 -u tools/timing_overhead.py unbound > $OUT/overhead_none.log 2>&1; }; rc=$?
               cat $OUT/overhead_near.log $OUT/overhead_none.log ;;
+    share2) BENCH_TEST_SHARE_GPU=1 timeout -k 10 300 python -u bench.py --gpus 2 --mib 64 --steps 10 --warmup 3 \
+                --collectives off > $OUT/bench_share2.log 2>&1; rc=$?; tail -c 1500 $OUT/bench_share2.log ;;
     rotate) timeout -k 10 400 tools/fold_rotate 9 > $OUT/fold_rotate.log 2>&1; rc=$?; cat $OUT/fold_rotate.log ;;
     *) echo "unknown step $step"; rc=2 ;;
     esac
