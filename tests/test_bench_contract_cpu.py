@@ -1,4 +1,4 @@
-"""The committed bench line (profiles/r06/bench_r06c.log, measured on MI355X) against
+"""The committed bench line (profiles/r06/bench_r06f.log, measured on MI355X) against
 the driver's contract and against itself: BASELINE.json's metric, the
 required keys, value = algorithmic bytes x N / time, roofline.frac =
 achieved / peak with achieved = 805,306,368 B / mean launch time, and the
@@ -10,7 +10,7 @@ import os
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LINE = os.path.join(ROOT, "profiles", "r06", "bench_r06c.log")
+LINE = os.path.join(ROOT, "profiles", "r06", "bench_r06f.log")
 GIB = float(1 << 30)
 
 
@@ -135,3 +135,14 @@ def test_build_id_in_line(line):
     """Round 6: the line names the sources its binaries came from."""
     bid = dict(kv.split("=", 1) for kv in line["config"]["build_id"].split())
     assert set(bid) == {"src", "tiles", "git"} and len(bid["src"]) == 16 and len(bid["tiles"]) == 16
+
+
+def test_call_split_in_line(line):
+    """Round 6: the profiled calls' split -- entry -> doorbell, the kernel (CP
+    clock), doorbell -> completion seen minus the kernel (neither depends on the
+    runtime's clock translation) -- and the timed region's cost outside the calls."""
+    sp = line["call_distribution"]["decomposition"]["split_medians"]
+    assert sp["calls"] == line["steps"]
+    assert 0 < sp["host_to_doorbell_us"] < 5 and 0 < sp["doorbell_to_seen_minus_kernel_us"] < 20
+    assert sp["kernel_us"] == pytest.approx(line["roofline"]["median_launch_us"], rel=0.03)
+    assert 0 < line["call_distribution"]["timed_region_outside_calls_us"] < 100
