@@ -641,6 +641,81 @@ struct DirectSignals {
 };
 thread_local DirectSignals t_sig;
 
+namespace {
+// A/B knob (tools/placement_ab.py; default off): MPIR_CVAR_REDUCE_LOCAL_SIGNAL_NODE=n
+// makes the completion signals of unprofiled direct calls amd_signal_t blocks
+// (amd_hsa_signal.h: the layout the CP decrements) that the library allocates
+// from the fine-grained pool of the n-th CPU agent (NUMA node n) and makes
+// accessible to the GPU, instead of the HSA runtime's own signals, so where the
+// signal lives can be chosen and measured.  No event mailbox: the caller polls.
+int signal_node_knob() {
+    static const int n = [] {
+        const char *e = getenv("MPIR_CVAR_REDUCE_LOCAL_SIGNAL_NODE");
+        return e && *e ? atoi(e) : -1;
+    }();
+    return n;
+}
+struct PoolFind {
+    int want, seen = 0;
+    hsa_agent_t cpu{};
+    bool found = false;
+    hsa_amd_memory_pool_t pool{};
+    bool have_pool = false;
+};
+hsa_status_t find_nth_cpu(hsa_agent_t a, void *p) {
+    PoolFind *f = static_cast<PoolFind *>(p);
+    hsa_device_type_t t;
+    if (hsa_agent_get_info(a, HSA_AGENT_INFO_DEVICE, &t) == HSA_STATUS_SUCCESS && t == HSA_DEVICE_TYPE_CPU) {
+        if (f->seen++ == f->want) {
+            f->cpu = a;
+            f->found = true;
+            return HSA_STATUS_INFO_BREAK;
+        }
+    }
+    return HSA_STATUS_SUCCESS;
+}
+hsa_status_t find_fine_pool(hsa_amd_memory_pool_t p, void *arg) {
+    PoolFind *f = static_cast<PoolFind *>(arg);
+    hsa_amd_segment_t seg;
+    uint32_t flags = 0;
+    bool alloc = false;
+    if (hsa_amd_memory_pool_get_info(p, HSA_AMD_MEMORY_POOL_INFO_SEGMENT, &seg) != HSA_STATUS_SUCCESS ||
+        seg != HSA_AMD_SEGMENT_GLOBAL)
+        return HSA_STATUS_SUCCESS;
+    hsa_amd_memory_pool_get_info(p, HSA_AMD_MEMORY_POOL_INFO_GLOBAL_FLAGS, &flags);
+    hsa_amd_memory_pool_get_info(p, HSA_AMD_MEMORY_POOL_INFO_RUNTIME_ALLOC_ALLOWED, &alloc);
+    if ((flags & HSA_AMD_MEMORY_POOL_GLOBAL_FLAG_FINE_GRAINED) && alloc) {
+        f->pool = p;
+        f->have_pool = true;
+        return HSA_STATUS_INFO_BREAK;
+    }
+    return HSA_STATUS_SUCCESS;
+}
+// this thread's placed signal for device dev (nullptr: not available)
+thread_local amd_signal_t *t_placed_sig[kMaxDirectDev] = {};
+amd_signal_t *placed_signal(int dev) {
+    if (t_placed_sig[dev]) return t_placed_sig[dev];
+    PoolFind f;
+    f.want = signal_node_knob();
+    hsa_iterate_agents(find_nth_cpu, &f);
+    if (!f.found) return nullptr;
+    hsa_amd_agent_iterate_memory_pools(f.cpu, find_fine_pool, &f);
+    if (!f.have_pool) return nullptr;
+    void *mem = nullptr;
+    if (hsa_amd_memory_pool_allocate(f.pool, 4096, 0, &mem) != HSA_STATUS_SUCCESS) return nullptr;
+    if (hsa_amd_agents_allow_access(1, &g_dev[dev].agent, nullptr, mem) != HSA_STATUS_SUCCESS) {
+        hsa_amd_memory_pool_free(mem);
+        return nullptr;
+    }
+    amd_signal_t *sg = static_cast<amd_signal_t *>(mem);
+    memset(sg, 0, sizeof *sg);
+    sg->kind = AMD_SIGNAL_KIND_USER;
+    sg->value = 0;
+    t_placed_sig[dev] = sg;     // (kept for the thread's life: 4 KiB per thread and device, test knob only)
+    return sg;
+}
+}  // namespace
+
 // ---- placement: where the synchronous call's host side runs relative to the
 // device.  The call's host-memory traffic is the doorbell write (MMIO to the
 // device's BAR), the completion signal the CP writes and the host polls, and
@@ -774,7 +849,8 @@ void direct_placement(int dev, int out[5]) {
     out[0] = cpu;
     out[1] = cpu_node(cpu);
     out[2] = dev >= 0 && dev < kMaxDirectDev ? device_node(dev) : -1;
-    out[3] = dev >= 0 && dev < kMaxDirectDev && t_sig.have[dev]
+    out[3] = dev >= 0 && dev < kMaxDirectDev && t_placed_sig[dev] ? page_node(t_placed_sig[dev])
+             : dev >= 0 && dev < kMaxDirectDev && t_sig.have[dev]
                  ? page_node(reinterpret_cast<const void *>((uintptr_t)t_sig.sig[dev].handle))
                  : -1;
     out[4] = dev >= 0 && dev < kMaxDirectDev && g_dev[dev].err ? page_node((const void *)g_dev[dev].err) : -1;
@@ -836,12 +912,15 @@ int direct_reduce(int dev, int op, int elem, const ReducePlan &p, int *rc) {
         }
     }
     hsa_signal_t sig;
-    if (!t_sig.get(dev, &sig)) return 0;
+    amd_signal_t *psig = !prof && signal_node_knob() >= 0 ? placed_signal(dev) : nullptr;
+    if (psig) sig.handle = (uint64_t)(uintptr_t)psig;
+    else if (!t_sig.get(dev, &sig)) return 0;
     uint64_t t_rung = 0;
     const uint32_t groups = (uint32_t)p.groups;
     const unsigned char *ka = p.args;
     const uint32_t kn = p.arg_bytes;
-    hsa_signal_store_relaxed(sig, 1);
+    if (psig) __atomic_store_n(&psig->value, (int64_t)1, __ATOMIC_RELAXED);
+    else hsa_signal_store_relaxed(sig, 1);
     CacheEntry *held = nullptr;
     int ring = -1;
     bool checked = true;
@@ -965,7 +1044,8 @@ int direct_reduce(int dev, int op, int elem, const ReducePlan &p, int *rc) {
     }
     if (t_rung)
         while (mono_ns() - t_rung < poll_cfg().delay_ns) _mm_pause();
-    for (uint64_t it = 1; hsa_signal_load_scacquire(sig) != 0; ++it) {
+    for (uint64_t it = 1; (psig ? __atomic_load_n(&psig->value, __ATOMIC_ACQUIRE) : hsa_signal_load_scacquire(sig)) != 0;
+         ++it) {
         if ((it & 0xFFFF) == 0 && d.queue_error.load(std::memory_order_relaxed)) {
             *rc = MPIR_HIP_ERUNTIME;
             return 1;       // (the entry stays held: a faulted queue is not used again)

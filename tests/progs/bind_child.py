@@ -1,6 +1,7 @@
 """Child of tests/test_bind_gpu.py: one synchronous device-resident
 MPI_Reduce_local with MPIR_CVAR_REDUCE_LOCAL_BIND as the parent set it; prints
-the calling thread's affinity before and after, and its placement."""
+the calling thread's affinity before and after, and its placement.
+BIND_CHILD_CALLS=n makes it n calls in a row (b += a each time)."""
 import json
 import os
 import sys
@@ -18,8 +19,11 @@ a = torch.ones(1 << 20, device="cuda")
 b = torch.ones(1 << 20, device="cuda")
 torch.cuda.synchronize()
 before = sorted(os.sched_getaffinity(0))
-rc = m.reduce_local(a.data_ptr(), b.data_ptr(), 1 << 20, m.MPI_FLOAT, m.MPI_SUM)
+calls = int(os.environ.get("BIND_CHILD_CALLS", "1"))
+rc = 0
+for _ in range(calls):
+    rc = rc or m.reduce_local(a.data_ptr(), b.data_ptr(), 1 << 20, m.MPI_FLOAT, m.MPI_SUM)
 after = sorted(os.sched_getaffinity(0))
-ok = bool(torch.all(b == 2).item())
+ok = bool(torch.all(b == 1 + calls).item())
 print(json.dumps({"rc": rc, "ok": ok, "before": before, "after": after, "placement": m.placement(0),
                   "direct": lib.MPIR_Hip_direct_dispatches()}))

@@ -25,6 +25,7 @@ def node_cpus(node):
 def run(env_extra):
     env = dict(os.environ)
     env.pop("MPIR_CVAR_REDUCE_LOCAL_BIND", None)
+    env.pop("MPIR_CVAR_REDUCE_LOCAL_SIGNAL_NODE", None)
     env.update(env_extra)
     p = subprocess.run([sys.executable, CHILD], capture_output=True, text=True, timeout=180, env=env)
     assert p.returncode == 0, p.stderr[-2000:]
@@ -49,3 +50,17 @@ def test_unset_leaves_affinity_alone():
     d = run({})
     assert d["rc"] == 0 and d["ok"]
     assert d["after"] == d["before"]
+
+
+def test_signal_node_knob():
+    """MPIR_CVAR_REDUCE_LOCAL_SIGNAL_NODE=0 (the placement A/B's knob): the
+    unprofiled calls complete on a signal the library allocated on node 0,
+    and results are unchanged."""
+    d = run({"MPIR_CVAR_REDUCE_LOCAL_SIGNAL_NODE": "0", "BIND_CHILD_CALLS": "50"})
+    assert d["rc"] == 0 and d["ok"] and d["direct"] >= 50
+    assert d["placement"]["signal_node"] in (0, -1)     # -1: the page's node not reported
+
+
+def test_signal_node_knob_missing_node_falls_back():
+    d = run({"MPIR_CVAR_REDUCE_LOCAL_SIGNAL_NODE": "99", "BIND_CHILD_CALLS": "20"})
+    assert d["rc"] == 0 and d["ok"] and d["direct"] >= 20

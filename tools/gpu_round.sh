@@ -16,8 +16,10 @@
 #   driver6    python bench.py --steps 20 --warmup 5 (the driver's shape), six fresh processes
 #   bench20    python bench.py --steps 20 --warmup 5, once (round 6: one bench pass per product change)
 #   classifyt  tests/test_classify_kinds_gpu.py (pointer kinds, kept verdicts)
+#   bindt      tests/test_bind_gpu.py (the binding and signal-node knobs)
 #   place      tools/placement_ab.py (near / far / as-launched caller, alternated processes)
 #   place2     the same with the waiting knobs (lazy / delay / flush polls) beside near and far
+#   place3     near / far callers with the completion signal on the GPU's node (sigg) or another (sigo)
 #   pipe       the collectives' GPU tests (loopback, config sizes, fused schedules)
 #   overlap    tools/pipeline_overlap (fold beside a one-rank RCCL transfer, serial vs overlapped, capped or not)
 #   pipeab     tools/pipeline_ab.py (config 5 through the loopback, pipelined vs not)
@@ -67,10 +69,14 @@ PY
              tail -c 3000 $OUT/bench20.log ;;
     classifyt) timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread \
                 tests/test_classify_kinds_gpu.py > $OUT/pytest_classify.log 2>&1; rc=$?; tail -4 $OUT/pytest_classify.log ;;
+    bindt) timeout -k 10 300 python -u -m pytest -x -v --timeout 180 --timeout-method thread \
+                tests/test_bind_gpu.py > $OUT/pytest_bind.log 2>&1; rc=$?; tail -6 $OUT/pytest_bind.log ;;
     place) timeout -k 10 600 python -u tools/placement_ab.py 4 2000 > $OUT/placement_ab.log 2>&1; rc=$?
            tail -8 $OUT/placement_ab.log ;;
     place2) timeout -k 10 900 python -u tools/placement_ab.py 3 2000 near,far,near:lazy,far:lazy,near:flush,near:delay \
                 > $OUT/placement_ab2.log 2>&1; rc=$?; tail -9 $OUT/placement_ab2.log ;;
+    place3) timeout -k 10 900 python -u tools/placement_ab.py 3 2000 near,near:sigg,near:sigo,far,far:sigg,far:sigo \
+              > $OUT/placement_sig.log 2>&1; rc=$?; tail -9 $OUT/placement_sig.log ;;
     pipe) timeout -k 10 400 python -u -m pytest -x -q --timeout 200 --timeout-method thread \
                 tests/test_coll_loopback_gpu.py tests/test_config_size_gpu.py tests/test_schedule_fused_gpu.py \
                 > $OUT/pytest_pipe.log 2>&1; rc=$?; tail -2 $OUT/pytest_pipe.log ;;

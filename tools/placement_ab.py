@@ -15,7 +15,10 @@ GPU's NUMA node ("near"), to the other node's ("far"), or left as launched
   * where everything sat: the thread's CPU / node, the GPU's node, the nodes of
     the completion signal and the error word (MPIR_Hip_direct_placement).
 
-    python3 tools/placement_ab.py [rounds] [k]     # parent: alternates the modes
+    python3 tools/placement_ab.py [rounds] [k] [modes]   # parent: alternates the modes
+modes: near | far | none, each optionally with suffixes ":lazy" ":delay" ":flush"
+(the waiting knobs) and ":sigg" / ":sigo" (the completion signal of unprofiled
+calls allocated on the GPU's node / on another node, MPIR_CVAR_REDUCE_LOCAL_SIGNAL_NODE).
 Output: one JSON line per process, then a summary table (medians over rounds).
 """
 import json
@@ -80,6 +83,14 @@ def child(mode: str, k: int) -> None:
     lib.MPIR_Hip_direct_prepare(0)
     gnode = m.placement(0)["gpu_node"]
     where = mode.split(":")[0]
+    sig = [x for x in mode.split(":")[1:] if x.startswith("sig")]
+    if sig and gnode >= 0:
+        # completion signal in the fine-grained pool of the GPU's node (sigg) or
+        # of another node (sigo): MPIR_CVAR_REDUCE_LOCAL_SIGNAL_NODE, read at the
+        # first direct call, which is below
+        others = [n for n in nodes() if n != gnode]
+        node = gnode if sig[0] == "sigg" else (others[0] if others else gnode)
+        os.environ["MPIR_CVAR_REDUCE_LOCAL_SIGNAL_NODE"] = str(node)
     allowed = os.sched_getaffinity(0)
     want = None
     if where == "near" and gnode >= 0:
@@ -108,10 +119,12 @@ def child(mode: str, k: int) -> None:
     st = np.zeros(k + 1, np.int64)
     assert loop(sets, 25, k, st) == 0
     long = stats(np.diff(st).tolist())
-    place = m.placement(0)
+    place = m.placement(0)      # (the signal node is that of the knob's signal when it is set)
     # the split of profiled calls (timestamped twin queue)
     import ctypes
     sp = (ctypes.c_uint64 * 4)()
+    # the profiled calls below use the runtime's signals; the knob's signal
+    # covers the unprofiled loops (window20, loop, small loop)
     lib.MPIR_Hip_direct_profile(1)
     rows = []
     try:
@@ -157,7 +170,8 @@ def child(mode: str, k: int) -> None:
                       "frac_at_median": round(3 * 256 * MIB / (long["median_us"] * 1e-6) / HBM, 4),
                       "frac_window20_mean": round(3 * 256 * MIB / (window["mean_us"] * 1e-6) / HBM, 4),
                       "split": split, "small_4KiB": {"loop": small_loop, "split": small_split},
-                      "env": {k: v for k, v in os.environ.items() if k.startswith("MPIR_CVAR_REDUCE_LOCAL_POLL")},
+                      "env": {k: v for k, v in os.environ.items() if k.startswith(("MPIR_CVAR_REDUCE_LOCAL_POLL",
+                                                                                   "MPIR_CVAR_REDUCE_LOCAL_SIGNAL"))},
                       "direct_state": lib.MPIR_Hip_direct_state(0)}), flush=True)
 
 
@@ -177,7 +191,9 @@ def main():
         order = modes[r % len(modes):] + modes[:r % len(modes)]
         for mode in order:
             t0 = time.time()
-            env = dict(os.environ, **WAITS[mode.split(":")[1] if ":" in mode else ""])
+            env = dict(os.environ)
+            for suffix in mode.split(":")[1:]:
+                env.update(WAITS.get(suffix, {}))
             p = subprocess.run([sys.executable, os.path.abspath(__file__), "--child", mode, str(k)],
                                capture_output=True, text=True, timeout=240, env=env)
             lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
