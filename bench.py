@@ -573,7 +573,8 @@ def bind_near_gpu(m, dev: int) -> dict:
     binding does for a GPU rank (Hydra -bind-to, Slurm --cpu-bind / numactl
     --cpunodebind).  Near against far callers, alternated fresh processes on one
     box (tools/placement_ab.py, DESIGN.md §(d) "Where the caller runs"): the
-    synchronous call ~2 us faster near.  BENCH_BIND=none keeps the placement the
+    synchronous call ~0.5 us faster near with the library's VRAM rings (~2 us
+    with ROCm's host-memory rings).  BENCH_BIND=none keeps the placement the
     process was launched with."""
     if os.environ.get("BENCH_BIND", "gpu-node") == "none":
         return {"mode": "none (as launched)"}
@@ -1215,7 +1216,8 @@ def main():
             variants["launch_placement"] = dict(
                 rate(launch_variant["dt"]), env="BENCH_BIND=none (child process): the calling thread where the "
                 "process was launched", placement=launch_variant.get("placement"),
-                fresh_args=rate(launch_variant["dt_fresh"]))
+                fresh_args=rate(launch_variant["dt_fresh"]),
+                HSA_ALLOCATE_QUEUE_DEV_MEM_seen=launch_variant.get("HSA_ALLOCATE_QUEUE_DEV_MEM"))
         else:
             variants["launch_placement"] = launch_variant
     out["sync_variants"] = variants

@@ -158,6 +158,13 @@ int MPIR_Hip_direct_state(int dev);
  * (Option 1).  Idempotent and thread-safe; returns
  * MPIR_Hip_direct_state(dev). */
 int MPIR_Hip_direct_prepare(int dev);
+
+/* The library's load-time default HSA_ALLOCATE_QUEUE_DEV_MEM=1 (AQL rings in
+ * VRAM), applied on request: 1 set now, 0 the environment already holds a
+ * value (kept), -1 the HSA runtime has started (too late, nothing done), -2 the
+ * process runs other threads and threads_ok is 0.  The constructor applies it
+ * with threads_ok 0; the Python package's load() with 1. */
+int MPIR_Hip_default_rings_in_vram(int threads_ok);
 /* With profiling on, the calling thread's last direct call on the system
  * clock, ns from entering the dispatch: doorbell rung, CP start, CP end,
  * completion seen by the host.  The CP's two stamps reach the system clock

@@ -591,15 +591,28 @@ int process_threads() {
     return n;
 }
 
-__attribute__((constructor)) void default_rings_in_vram() {
-    if (getenv("HSA_ALLOCATE_QUEUE_DEV_MEM")) return;
+// 1 set now, 0 the environment holds a value, -1 the HSA runtime has started,
+// -2 the process runs other threads and `threads_ok` is 0.
+int rings_default(int threads_ok) {
+    if (getenv("HSA_ALLOCATE_QUEUE_DEV_MEM")) return 0;
     uint16_t major = 0;
-    if (hsa_system_get_info(HSA_SYSTEM_INFO_VERSION_MAJOR, &major) == HSA_STATUS_SUCCESS) return;
-    if (process_threads() != 1) return;
+    if (hsa_system_get_info(HSA_SYSTEM_INFO_VERSION_MAJOR, &major) == HSA_STATUS_SUCCESS) return -1;
+    if (!threads_ok && process_threads() != 1) return -2;
     setenv("HSA_ALLOCATE_QUEUE_DEV_MEM", "1", 0);
+    return 1;
 }
 
+__attribute__((constructor)) void default_rings_in_vram() { (void)rings_default(0); }
+
 }  // namespace
+
+// The same default, asked for by a caller that knows its other threads leave
+// the environment alone -- the Python package's load(): an interpreter that
+// imported numpy or torch first already runs their (parked) pool threads, so
+// the constructor above stood aside, and without this its queues keep ROCm's
+// host-memory rings, ~0.7 us on every synchronous call (tools/aql/cp_floor.sh,
+// profiles/r06/cp_floor_r06j.log).
+extern "C" int MPIR_Hip_default_rings_in_vram(int threads_ok) { return rings_default(threads_ok); }
 
 // Completion signals, one per (thread, device).  A thread's signals go back
 // to a process-wide free list when it exits (no HSA call at thread exit) and

@@ -123,6 +123,7 @@ EXPORTED_SYMBOLS = [
     "MPIR_Hip_direct_last_kernel_ns", "MPIR_Hip_direct_state", "MPIR_Hip_direct_busy_skips",
     "MPIR_Hip_direct_last_split", "MPIR_Hip_direct_kernarg_writes", "MPIR_Hip_direct_placement", "MPIR_Hip_build_id", "MPIR_Hip_combine_set_flags",
     "MPIR_Hip_direct_prepare", "MPIR_Hip_set_local_ranks", "MPIR_Hip_host_threads",
+    "MPIR_Hip_default_rings_in_vram",
     # runtime subset for config 1 (include/mpi_pip.h)
     "MPI_Init", "MPI_Initialized", "MPI_Finalize", "MPI_Finalized", "MPI_Abort", "MPI_Comm_size",
     "MPI_Comm_rank", "MPI_Get_processor_name", "MPI_Wtime", "MPI_Wtick", "MPI_Barrier", "MPI_Bcast",
@@ -133,6 +134,11 @@ MPI_User_function = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_void_p,
                                      ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int))
 
 _lib = None
+
+
+# what load()'s MPIR_Hip_default_rings_in_vram(1) returned: 1 set then, 0 the
+# environment held a value, -1 the HSA runtime had started (None: not loaded)
+RINGS_DEFAULT = None
 
 
 def load(path: str | None = None) -> ctypes.CDLL:
@@ -208,6 +214,8 @@ def load(path: str | None = None) -> ctypes.CDLL:
     lib.MPIR_Hip_direct_placement.restype = None
     lib.MPIR_Hip_direct_prepare.argtypes = [i32]
     lib.MPIR_Hip_direct_prepare.restype = i32
+    lib.MPIR_Hip_default_rings_in_vram.argtypes = [i32]
+    lib.MPIR_Hip_default_rings_in_vram.restype = i32
     lib.MPIR_Hip_set_local_ranks.argtypes = [i32]
     lib.MPIR_Hip_set_local_ranks.restype = i32
     lib.MPIR_Hip_host_threads.argtypes = []
@@ -222,6 +230,15 @@ def load(path: str | None = None) -> ctypes.CDLL:
         f = getattr(lib, name)
         f.argtypes = [i32]
         f.restype = i32
+    # AQL rings in VRAM (direct_dispatch.hip default_rings_in_vram): the load-time
+    # constructor stands aside in a process that already runs threads, which an
+    # interpreter that imported numpy or torch first does (their pools are
+    # parked and leave the environment alone); load() applies the default then,
+    # while the HSA runtime has not started and the job set no value.
+    global RINGS_DEFAULT
+    RINGS_DEFAULT = lib.MPIR_Hip_default_rings_in_vram(1)
+    if RINGS_DEFAULT == 1:
+        os.environ["HSA_ALLOCATE_QUEUE_DEV_MEM"] = "1"      # Python's view of the variable the library set
     if path is None:
         _lib = lib
     return lib

@@ -4,7 +4,7 @@
 //
 //   g++ -O2 -std=c++17 -I/opt/rocm/include tools/aql/cp_latency.cpp -o tools/aql/cp_latency \
 //       -L/opt/rocm/lib -lhsa-runtime64 -Wl,-rpath,/opt/rocm/lib
-//   [HSA_ALLOCATE_QUEUE_DEV_MEM=1] tools/aql/cp_latency mpich-pip_amd/lib/libmpir_hip_tiles.hsaco
+//   [HSA_ALLOCATE_QUEUE_DEV_MEM=1] [KARG_VRAM=1] [IDLE_ONLY=1] [EXTRA_QUEUES=n] [HIP_INIT=1] tools/aql/cp_latency mpich-pip_amd/lib/libmpir_hip_tiles.hsaco
 //
 // Cases (medians over 300 calls, us; all on the system timestamp clock):
 //   idle G      one dispatch, the host idles G us after the previous completion
@@ -17,6 +17,7 @@
 //               dispatch behind it, rings, then sets the flag: flag -> CP start
 #include <hsa/hsa.h>
 #include <hsa/hsa_ext_amd.h>
+#include <dlfcn.h>
 #include <immintrin.h>
 
 #include <algorithm>
@@ -150,9 +151,30 @@ static double med(std::vector<double> v) {
     return v[v.size() / 2];
 }
 
+// HIP_INIT=1: bring the HIP runtime up in this process first (as the library's
+// callers have it): hipInit, a 1 GiB hipMalloc, a hipMemset on the null stream
+// and a synchronize, through dlopen so the tool keeps building without HIP.
+static void hip_init() {
+    void *h = dlopen("libamdhip64.so", RTLD_NOW | RTLD_GLOBAL);
+    if (!h) { printf("dlopen libamdhip64: %s\n", dlerror()); exit(3); }
+    auto init = (int (*)(unsigned))dlsym(h, "hipInit");
+    auto setdev = (int (*)(int))dlsym(h, "hipSetDevice");
+    auto mal = (int (*)(void **, size_t))dlsym(h, "hipMalloc");
+    auto mset = (int (*)(void *, int, size_t))dlsym(h, "hipMemset");
+    auto sync = (int (*)())dlsym(h, "hipDeviceSynchronize");
+    void *p = nullptr;
+    if (!init || !setdev || !mal || !mset || !sync || init(0) || setdev(0) || mal(&p, 1ull << 30) ||
+        mset(p, 0, 1ull << 30) || sync()) {
+        printf("HIP bring-up failed\n");
+        exit(3);
+    }
+    printf("HIP runtime up (1 GiB allocated and set)\n");
+}
+
 int main(int argc, char **argv) {
     if (argc < 2) { printf("usage: %s tiles.hsaco\n", argv[0]); return 1; }
     setvbuf(stdout, nullptr, _IOLBF, 0);
+    if (getenv("HIP_INIT")) hip_init();
     HK(hsa_init());
     HK(hsa_iterate_agents(find_agents, nullptr));
     hsa_amd_agent_iterate_memory_pools(g_gpu, find_vram, nullptr);
@@ -179,10 +201,21 @@ int main(int argc, char **argv) {
     // operands (16 KiB each, VRAM) and kernargs (kernarg pool, host memory)
     void *dev = nullptr;
     HK(hsa_amd_memory_pool_allocate(g_vram, 1 << 16, 0, &dev));
-    HK(hsa_amd_memory_pool_allocate(g_kern, 64, 0, &g_karg));
-    HK(hsa_amd_agents_allow_access(1, &g_gpu, nullptr, g_karg));
     KArgs ka{(const char *)dev, (char *)dev + 32768, 16384, 0};
-    memcpy(g_karg, &ka, sizeof ka);
+    if (getenv("KARG_VRAM")) {
+        // KARG_VRAM=1: the kernargs in VRAM, as the library keeps its slots
+        // (written once by a copy, so the first dispatch already sees them)
+        HK(hsa_amd_memory_pool_allocate(g_vram, 4096, 0, &g_karg));
+        char tmp[128] = {};
+        memcpy(tmp, &ka, sizeof ka);
+        HK(hsa_memory_copy(g_karg, tmp, sizeof tmp));
+    } else {
+        HK(hsa_amd_memory_pool_allocate(g_kern, 128, 0, &g_karg));
+        HK(hsa_amd_agents_allow_access(1, &g_gpu, nullptr, g_karg));
+        memset(g_karg, 0, 128);
+        memcpy(g_karg, &ka, sizeof ka);
+    }
+    printf("kernargs in %s\n", getenv("KARG_VRAM") ? "VRAM" : "the kernarg pool (host memory)");
     // QUEUE_SINGLE=1: a single-producer queue; QUEUE_SIZE: packets in the ring
     const uint32_t qsize = getenv("QUEUE_SIZE") ? (uint32_t)atoi(getenv("QUEUE_SIZE")) : 1024u;
     const hsa_queue_type32_t qtype = getenv("QUEUE_SINGLE") ? HSA_QUEUE_TYPE_SINGLE : HSA_QUEUE_TYPE_MULTI;
@@ -196,6 +229,28 @@ int main(int argc, char **argv) {
         HK(hsa_amd_queue_set_priority(g_q, qp));
         printf("queue priority %s\n", pr);
     }
+    // EXTRA_QUEUES=n: n more (idle) queues on the GPU, each with one dispatch
+    // run through it first, as other streams of the same process would leave them
+    const int extra = getenv("EXTRA_QUEUES") ? atoi(getenv("EXTRA_QUEUES")) : 0;
+    for (int i = 0; i < extra; ++i) {
+        hsa_queue_t *q2;
+        HK(hsa_queue_create(g_gpu, 256, HSA_QUEUE_TYPE_MULTI, nullptr, nullptr, UINT32_MAX, UINT32_MAX, &q2));
+        hsa_signal_t sx;
+        HK(hsa_signal_create(1, 0, nullptr, &sx));
+        hsa_queue_t *keep = g_q;
+        g_q = q2;
+        const uint64_t idx = hsa_queue_load_write_index_relaxed(g_q);
+        write_dispatch(idx, sx, true);
+        hsa_queue_store_write_index_relaxed(g_q, idx + 1);
+        hsa_signal_store_screlease(g_q->doorbell_signal, idx);
+        g_q = keep;
+        const uint64_t t0 = ts();
+        while (hsa_signal_load_scacquire(sx) != 0) {
+            if (us(ts() - t0) > 2e6) { printf("extra queue dispatch timed out\n"); return 4; }
+        }
+        hsa_signal_destroy(sx);
+    }
+    if (extra) printf("%d extra queues\n", extra);
     hsa_signal_t s1, s2;
     HK(hsa_signal_create(0, 1, &g_gpu, &s1));
     HK(hsa_signal_create(0, 1, &g_gpu, &s2));
@@ -266,6 +321,7 @@ int main(int argc, char **argv) {
         printf("idle %7.1f us: doorbell->CP start %5.2f  CP start->end %5.2f  CP end->host sees %5.2f  doorbell->host sees %5.2f\n",
                G, med(d2s), med(s2e), med(e2h), med(tot));
     }
+    if (getenv("IDLE_ONLY")) return 0;
     // pair
     {
         std::vector<double> gap, d2s;
