@@ -1,4 +1,4 @@
-"""The committed bench line (profiles/r06/bench_r06f.log, measured on MI355X) against
+"""The committed bench line (profiles/r06/bench_r06l_ds.log, measured on MI355X) against
 the driver's contract and against itself: BASELINE.json's metric, the
 required keys, value = algorithmic bytes x N / time, roofline.frac =
 achieved / peak with achieved = 805,306,368 B / mean launch time, and the
@@ -10,7 +10,7 @@ import os
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LINE = os.path.join(ROOT, "profiles", "r06", "bench_r06f.log")
+LINE = os.path.join(ROOT, "profiles", "r06", "bench_r06l_ds.log")
 GIB = float(1 << 30)
 
 
@@ -129,6 +129,10 @@ def test_placement_recorded_and_bound(line):
     lp = line["sync_variants"]["launch_placement"]
     assert lp["value"] > 0 and lp["placement"]["gpu_node"] == vc["gpu_node"]
     assert "BENCH_BIND=none" in lp["env"]
+    # since r06l the child's AQL rings are the library's (VRAM), like the main loop's:
+    # the comparison is the placement's alone (DESIGN.md §(d), "Where the caller runs")
+    assert lp["HSA_ALLOCATE_QUEUE_DEV_MEM_seen"] == "1"
+    assert line["config"]["runtime"]["HSA_ALLOCATE_QUEUE_DEV_MEM"] == "1"
 
 
 def test_build_id_in_line(line):
