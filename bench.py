@@ -300,6 +300,7 @@ def time_loop(run, k: int, w: int, sync, barrier, max_over_ranks, own: list | No
         run(w, k)
     else:
         run(w, k, stamps)
+    tm = time.perf_counter()
     sync()
     t1 = time.perf_counter()
     if gc_on:
@@ -308,7 +309,7 @@ def time_loop(run, k: int, w: int, sync, barrier, max_over_ranks, own: list | No
     if bracket is not None and stamps is not None:
         # the timed region around the K calls: the Python -> C loop entry and
         # exit and the closing torch.cuda.synchronize() (same clock)
-        bracket.append((t1 - t0) - (int(stamps[k]) - int(stamps[0])) * 1e-9)
+        bracket.append(((t1 - t0) - (int(stamps[k]) - int(stamps[0])) * 1e-9, t1 - tm))
     if own is not None:
         own.append(t1 - t0)
     if calls is not None:
@@ -1113,7 +1114,8 @@ def main():
         if gap:
             cstats["idle_gap_before_first_us"] = round(gap[0] * 1e6, 1)
         if bracket:
-            cstats["timed_region_outside_calls_us"] = round(bracket[0] * 1e6, 2)
+            cstats["timed_region_outside_calls_us"] = round(bracket[0][0] * 1e6, 2)
+            cstats["timed_region_closing_sync_us"] = round(bracket[0][1] * 1e6, 2)
     direct_share = (lib.MPIR_Hip_direct_dispatches() - d_before) / ((3 if c_loop else 2) * (args.steps + args.warmup))
     value = alg_bytes * args.steps * world / dt / GIB
     # each rank's own figures beside the max-over-ranks `value`: a lagging GPU,

@@ -706,8 +706,10 @@ hsa_status_t find_fine_pool(hsa_amd_memory_pool_t p, void *arg) {
 }
 // this thread's placed signal for device dev (nullptr: not available)
 thread_local amd_signal_t *t_placed_sig[kMaxDirectDev] = {};
+thread_local bool t_placed_failed[kMaxDirectDev] = {};
 amd_signal_t *placed_signal(int dev) {
-    if (t_placed_sig[dev]) return t_placed_sig[dev];
+    if (t_placed_sig[dev] || t_placed_failed[dev]) return t_placed_sig[dev];
+    t_placed_failed[dev] = true;    // until the allocation below succeeds: tried once per thread
     PoolFind f;
     f.want = signal_node_knob();
     hsa_iterate_agents(find_nth_cpu, &f);
@@ -725,6 +727,7 @@ amd_signal_t *placed_signal(int dev) {
     sg->kind = AMD_SIGNAL_KIND_USER;
     sg->value = 0;
     t_placed_sig[dev] = sg;     // (kept for the thread's life: 4 KiB per thread and device, test knob only)
+    t_placed_failed[dev] = false;
     return sg;
 }
 }  // namespace
