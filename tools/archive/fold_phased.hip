@@ -1,5 +1,5 @@
 // fold_phased.hip -- does the 8-operand fold lose its ~6 points to the DRAM's
-// read/write turnarounds?  (DESIGN.md §(f), "Where the fold's time goes".)
+// read/write turnarounds?  (HISTORY.md, "Fused-fold experiments", round 5.)
 //
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off \
 //         -Impich-pip_amd/csrc/hip -o tools/archive/fold_phased tools/archive/fold_phased.hip
