@@ -446,7 +446,8 @@ def variant_child(args) -> None:
     print(json.dumps({"dt": dt, "dt_fresh": dtf, "kernarg_writes_per_fresh_call": writes,
                       "HSA_ALLOCATE_QUEUE_DEV_MEM": process_env("HSA_ALLOCATE_QUEUE_DEV_MEM"),
                       "direct_state": lib.MPIR_Hip_direct_state(0), "bind": bind,
-                      "placement": {k: place[k] for k in ("cpu", "cpu_node", "gpu_node")}}), flush=True)
+                      "placement": {k: place[k] for k in ("cpu", "cpu_node", "gpu_node", "ring_in_vram")}}),
+          flush=True)
 
 
 def run_variant_child(args, env_over: dict | None = None) -> dict:
@@ -1126,7 +1127,8 @@ def main():
                         direct_share, cstats["median_us"], cstats["p10_us"], cstats["p90_us"],
                         cstats["slow_share"], float(place_before["cpu"]), float(place["cpu"]),
                         float(place["cpu_node"]), float(place["gpu_node"]), float(place["signal_node"]),
-                        float(place["error_word_node"]), float(place["allowed_cpus"])], world, dist,
+                        float(place["error_word_node"]), float(place["allowed_cpus"]),
+                        float(place["ring_in_vram"])], world, dist,
                        "cpu" if pg_backend == "gloo" else "cuda")
 
     def rate(seconds):
@@ -1191,7 +1193,8 @@ def main():
                       "call_median_us": r[6], "call_p10_p90_us": [r[7], r[8]], "slow_share": r[9],
                       "placement": {"cpu_before_loop": int(r[10]), "cpu_after_loop": int(r[11]),
                                     "cpu_node": int(r[12]), "gpu_node": int(r[13]), "signal_node": int(r[14]),
-                                    "error_word_node": int(r[15]), "allowed_cpus": int(r[16])}}
+                                    "error_word_node": int(r[15]), "allowed_cpus": int(r[16]),
+                                    "ring_in_vram": int(r[17])}}
                      for r in rows],
         # rank 0's K timed calls, each on its own (clock stamps in the C loop)
         "call_distribution": dict(cstats, source="CLOCK_MONOTONIC after each call of the timed C loop (rank 0)"
@@ -1210,6 +1213,7 @@ def main():
                 "env": "HSA_ALLOCATE_QUEUE_DEV_MEM=0 (child process)",
                 "cached_args": rate(ring_variant["dt"]), "fresh_args": rate(ring_variant["dt_fresh"]),
                 "HSA_ALLOCATE_QUEUE_DEV_MEM_seen": ring_variant.get("HSA_ALLOCATE_QUEUE_DEV_MEM"),
+                "ring_in_vram": (ring_variant.get("placement") or {}).get("ring_in_vram"),
                 "direct_state": ring_variant.get("direct_state")}
         else:
             variants["rocm_ring_placement"] = ring_variant

@@ -196,6 +196,10 @@ void MPIR_Hip_direct_test_fail_probe(void);
  * this thread's completion signal for dev, out[4] the node of the device's
  * error word; -1 where unknown or not yet created. */
 void MPIR_Hip_direct_placement(int dev, int out[5]);
+/* Where device dev's direct-path queue keeps its AQL ring (diagnostic): 1 device
+ * memory (HSA_ALLOCATE_QUEUE_DEV_MEM=1, the library's default), 0 host memory,
+ * -1 no queue yet / unknown. */
+int MPIR_Hip_direct_ring_location(int dev);
 int MPIR_Hip_thread_contexts(void);
 
 /* The build id of this library: "src=<hash of csrc/ and include/> tiles=<hash

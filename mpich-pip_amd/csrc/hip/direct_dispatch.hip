@@ -872,6 +872,21 @@ void direct_placement(int dev, int out[5]) {
     out[4] = dev >= 0 && dev < kMaxDirectDev && g_dev[dev].err ? page_node((const void *)g_dev[dev].err) : -1;
 }
 
+// Where device dev's direct-path queue keeps its AQL ring: 1 in device memory,
+// 0 in host memory, -1 no queue yet or not an HSA allocation (diagnostic; the
+// bench records it per rank, DESIGN.md §(d) "Where the caller runs").
+extern "C" int MPIR_Hip_direct_ring_location(int dev) {
+    if (dev < 0 || dev >= kMaxDirectDev || !g_dev[dev].queue) return -1;
+    hsa_amd_pointer_info_t info{};
+    info.size = sizeof info;
+    if (hsa_amd_pointer_info(g_dev[dev].queue->base_address, &info, nullptr, nullptr, nullptr) != HSA_STATUS_SUCCESS ||
+        info.type != HSA_EXT_POINTER_TYPE_HSA)
+        return -1;
+    hsa_device_type_t t;
+    if (hsa_agent_get_info(info.agentOwner, HSA_AGENT_INFO_DEVICE, &t) != HSA_STATUS_SUCCESS) return -1;
+    return t == HSA_DEVICE_TYPE_GPU ? 1 : 0;
+}
+
 // How the caller waits for the completion signal (A/B knobs for
 // tools/placement_ab.py; the defaults are the product's):
 //   MPIR_CVAR_REDUCE_LOCAL_POLL_DELAY_US  spin on the clock, without reading

@@ -123,7 +123,7 @@ EXPORTED_SYMBOLS = [
     "MPIR_Hip_direct_last_kernel_ns", "MPIR_Hip_direct_state", "MPIR_Hip_direct_busy_skips",
     "MPIR_Hip_direct_last_split", "MPIR_Hip_direct_kernarg_writes", "MPIR_Hip_direct_placement", "MPIR_Hip_build_id", "MPIR_Hip_combine_set_flags",
     "MPIR_Hip_direct_prepare", "MPIR_Hip_set_local_ranks", "MPIR_Hip_host_threads",
-    "MPIR_Hip_default_rings_in_vram",
+    "MPIR_Hip_default_rings_in_vram", "MPIR_Hip_direct_ring_location",
     # runtime subset for config 1 (include/mpi_pip.h)
     "MPI_Init", "MPI_Initialized", "MPI_Finalize", "MPI_Finalized", "MPI_Abort", "MPI_Comm_size",
     "MPI_Comm_rank", "MPI_Get_processor_name", "MPI_Wtime", "MPI_Wtick", "MPI_Barrier", "MPI_Bcast",
@@ -216,6 +216,8 @@ def load(path: str | None = None) -> ctypes.CDLL:
     lib.MPIR_Hip_direct_prepare.restype = i32
     lib.MPIR_Hip_default_rings_in_vram.argtypes = [i32]
     lib.MPIR_Hip_default_rings_in_vram.restype = i32
+    lib.MPIR_Hip_direct_ring_location.argtypes = [i32]
+    lib.MPIR_Hip_direct_ring_location.restype = i32
     lib.MPIR_Hip_set_local_ranks.argtypes = [i32]
     lib.MPIR_Hip_set_local_ranks.restype = i32
     lib.MPIR_Hip_host_threads.argtypes = []
@@ -252,10 +254,13 @@ def build_id() -> str:
 def placement(dev: int = 0) -> dict:
     """MPIR_Hip_direct_placement for the calling thread: its CPU and NUMA node,
     device `dev`'s node, and the nodes of this thread's completion signal and of
-    the device's error word (-1 where unknown or not yet created)."""
+    the device's error word (-1 where unknown or not yet created); `ring_in_vram`:
+    MPIR_Hip_direct_ring_location (1 device memory, 0 host memory, -1 no queue)."""
+    lib = load()
     out = (ctypes.c_int * 5)()
-    load().MPIR_Hip_direct_placement(dev, out)
-    return {"cpu": out[0], "cpu_node": out[1], "gpu_node": out[2], "signal_node": out[3], "error_word_node": out[4]}
+    lib.MPIR_Hip_direct_placement(dev, out)
+    return {"cpu": out[0], "cpu_node": out[1], "gpu_node": out[2], "signal_node": out[3], "error_word_node": out[4],
+            "ring_in_vram": lib.MPIR_Hip_direct_ring_location(dev)}
 
 
 def error_class(code: int) -> int:

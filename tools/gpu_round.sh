@@ -22,6 +22,7 @@
 #   place3     near / far callers with the completion signal on the GPU's node (sigg) or another (sigo)
 #   cpfloor    tools/aql/cp_floor.sh (the CP's doorbell -> start floor with HSA alone, then the product's split)
 #   ccd        tools/ccd_ab.py (the calling thread moved across L3 domains in one process)
+#   pairalloc  tools/pair_alloc_ab.py --ab (per-pair call and kernel medians under four allocation methods)
 #   pipe       the collectives' GPU tests (loopback, config sizes, fused schedules)
 #   overlap    tools/pipeline_overlap (fold beside a one-rank RCCL transfer, serial vs overlapped, capped or not)
 #   pipeab     tools/pipeline_ab.py (config 5 through the loopback, pipelined vs not)
@@ -81,6 +82,7 @@ PY
               > $OUT/placement_sig.log 2>&1; rc=$?; tail -9 $OUT/placement_sig.log ;;
     cpfloor) timeout -k 10 600 bash tools/aql/cp_floor.sh > $OUT/cp_floor.log 2>&1; rc=$?; grep -v '^{' $OUT/cp_floor.log | tail -30 ;;
     ccd) timeout -k 10 300 python -u tools/ccd_ab.py 20 > $OUT/ccd_ab.log 2>&1; rc=$?; grep -v '^{"round' $OUT/ccd_ab.log | tail -24 ;;
+    pairalloc) timeout -k 10 600 python -u tools/pair_alloc_ab.py --ab 3 > $OUT/pair_alloc_ab.log 2>&1; rc=$?; tail -6 $OUT/pair_alloc_ab.log ;;
     pipe) timeout -k 10 400 python -u -m pytest -x -q --timeout 200 --timeout-method thread \
                 tests/test_coll_loopback_gpu.py tests/test_config_size_gpu.py tests/test_schedule_fused_gpu.py \
                 > $OUT/pytest_pipe.log 2>&1; rc=$?; tail -2 $OUT/pytest_pipe.log ;;
