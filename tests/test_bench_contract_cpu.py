@@ -1,4 +1,4 @@
-"""The committed bench line (profiles/r06/bench_r06l_ds.log, measured on MI355X) against
+"""The committed bench line (profiles/r06/bench_r06p_ds.log, measured on MI355X) against
 the driver's contract and against itself: BASELINE.json's metric, the
 required keys, value = algorithmic bytes x N / time, roofline.frac =
 achieved / peak with achieved = 805,306,368 B / mean launch time, and the
@@ -10,7 +10,7 @@ import os
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LINE = os.path.join(ROOT, "profiles", "r06", "bench_r06l_ds.log")
+LINE = os.path.join(ROOT, "profiles", "r06", "bench_r06p_ds.log")
 GIB = float(1 << 30)
 
 
@@ -124,6 +124,7 @@ def test_placement_recorded_and_bound(line):
                   "allowed_cpus"):
             assert k in pl, k
         assert pl["gpu_node"] >= 0 and pl["cpu_node"] == pl["gpu_node"]      # bound near its GPU
+        assert pl["ring_in_vram"] == 1          # the library's AQL ring in device memory
     vc = line["value_conditions"]["placement"]
     assert vc["mode"] == "gpu-node" and vc["gpu_node"] == line["per_rank"][0]["placement"]["gpu_node"]
     lp = line["sync_variants"]["launch_placement"]
