@@ -241,6 +241,12 @@ def load(path: str | None = None) -> ctypes.CDLL:
     RINGS_DEFAULT = lib.MPIR_Hip_default_rings_in_vram(1)
     if RINGS_DEFAULT == 1:
         os.environ["HSA_ALLOCATE_QUEUE_DEV_MEM"] = "1"      # Python's view of the variable the library set
+    elif RINGS_DEFAULT == -1 and path is None:
+        import warnings
+        warnings.warn("mpich_pip_amd loaded after the GPU runtime started: its AQL rings stay in host memory "
+                      "(~1.7 us per synchronous call); load it before the first GPU call, or export "
+                      "HSA_ALLOCATE_QUEUE_DEV_MEM=1 (INTEGRATION.md, 'Keep the AQL rings in VRAM')",
+                      RuntimeWarning, stacklevel=2)
     if path is None:
         _lib = lib
     return lib
