@@ -277,20 +277,32 @@ def time_loop(run, k: int, w: int, sync, barrier, max_over_ranks, own: list | No
     over a process group takes longer than that, so without it the first timed
     call would pay a wake-up that back-to-back calls never see."""
     late = w > 0 and os.environ.get("BENCH_WARMUP_ORDER", "late") != "before"
-    run(0, w - 1 if late else w)
+    stamps = wst = None
+    if calls is not None:
+        import numpy as np
+        stamps = np.zeros(k + 1, np.int64)
+        # the warm-up steps take the stamped path of the C loop too: its first
+        # use (the buffer protocol on the stamps array) otherwise lands inside
+        # the timed region (~2.3 us once, measured r06u: timed_region_loop_entry_us)
+        wst = np.zeros(w + 1, np.int64)
+
+    def warm(start, n):
+        if wst is None:
+            run(start, n)
+        else:
+            run(start, n, wst)
+    warm(0, w - 1 if late else w)
     if late:
         sync()
         barrier()
-        run(w - 1, 1)
+        warm(w - 1, 1)
     warm_end = time.monotonic_ns()         # CLOCK_MONOTONIC, the C loop's clock
     if not late:
         sync()
         barrier()
+    ts0 = time.perf_counter()
     sync()
-    stamps = None
-    if calls is not None:
-        import numpy as np
-        stamps = np.zeros(k + 1, np.int64)
+    ts1 = time.perf_counter()
     # Python's cyclic collector held off while the K calls run, as in
     # time_steps (and timeit)
     gc_on = gc.isenabled()
@@ -309,7 +321,10 @@ def time_loop(run, k: int, w: int, sync, barrier, max_over_ranks, own: list | No
     if bracket is not None and stamps is not None:
         # the timed region around the K calls: the Python -> C loop entry and
         # exit and the closing torch.cuda.synchronize() (same clock)
-        bracket.append(((t1 - t0) - (int(stamps[k]) - int(stamps[0])) * 1e-9, t1 - tm))
+        # (perf_counter is CLOCK_MONOTONIC on Linux, the stamps' clock: the
+        # entry into and the exit from the C loop split out)
+        bracket.append(((t1 - t0) - (int(stamps[k]) - int(stamps[0])) * 1e-9, t1 - tm,
+                        int(stamps[0]) * 1e-9 - t0, tm - int(stamps[k]) * 1e-9, ts1 - ts0))
     if own is not None:
         own.append(t1 - t0)
     if calls is not None:
@@ -1117,6 +1132,10 @@ def main():
         if bracket:
             cstats["timed_region_outside_calls_us"] = round(bracket[0][0] * 1e6, 2)
             cstats["timed_region_closing_sync_us"] = round(bracket[0][1] * 1e6, 2)
+            if time.get_clock_info("perf_counter").implementation.startswith("clock_gettime(CLOCK_MONOTONIC"):
+                cstats["timed_region_loop_entry_us"] = round(bracket[0][2] * 1e6, 2)
+                cstats["timed_region_loop_exit_us"] = round(bracket[0][3] * 1e6, 2)
+            cstats["opening_sync_us"] = round(bracket[0][4] * 1e6, 2)      # before t0, outside the region
     direct_share = (lib.MPIR_Hip_direct_dispatches() - d_before) / ((3 if c_loop else 2) * (args.steps + args.warmup))
     value = alg_bytes * args.steps * world / dt / GIB
     # each rank's own figures beside the max-over-ranks `value`: a lagging GPU,
