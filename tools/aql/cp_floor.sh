@@ -6,6 +6,8 @@
 # GPU's NUMA node (CP_FLOOR_EXTRA: the extra-queue counts, default 0), with the HIP
 # runtime absent and up; then the library from C (tools/aql/product_split) and
 # the product's own 4 KiB call split on the same box (tools/placement_ab.py, near).
+# CP_FLOOR_MODE=noprof: the bare client with and without CP timestamps beside the
+# library from C instead.
 # Build: the g++ line in tools/aql/cp_latency.cpp's header.
 set -o pipefail
 cd ${GRAFT_REPO_ROOT:-$PWD}
@@ -22,6 +24,20 @@ for part in '$cpus'.split(','):
     x,_,y=part.partition('-'); s.update(range(int(x), int(y or x)+1))
 print(','.join(map(str, sorted(a & s))) or '$allowed')")
 echo "GPU node $node; caller CPUs $pick"
+if [ "$CP_FLOOR_MODE" = noprof ]; then
+  # the library's queue runs without CP timestamps: the bare client with and
+  # without them (host clock only), then the library from C, twice, alternated
+  for r in 1 2; do
+    for np in 0 1; do
+      echo "== HIP up, ring and kernargs in VRAM, NO_PROFILE=$np"
+      env HSA_ALLOCATE_QUEUE_DEV_MEM=1 IDLE_ONLY=1 KARG_VRAM=1 HIP_INIT=1 $([ $np = 1 ] && echo NO_PROFILE=1) \
+          timeout -k 5 120 taskset -c $pick tools/aql/cp_latency mpich-pip_amd/lib/libmpir_hip_tiles.hsaco || exit $?
+    done
+    echo "== the product from C, no torch"
+    timeout -k 5 120 taskset -c $pick tools/aql/product_split 4096 || exit $?
+  done
+  exit 0
+fi
 for ring in 0 1; do
   for karg in 0 1; do
     [ "$CP_FLOOR_PLACEMENTS" = 1 ] || [ $ring$karg = 11 ] || continue

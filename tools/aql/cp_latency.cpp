@@ -4,7 +4,7 @@
 //
 //   g++ -O2 -std=c++17 -I/opt/rocm/include tools/aql/cp_latency.cpp -o tools/aql/cp_latency \
 //       -L/opt/rocm/lib -lhsa-runtime64 -Wl,-rpath,/opt/rocm/lib
-//   [HSA_ALLOCATE_QUEUE_DEV_MEM=1] [KARG_VRAM=1] [IDLE_ONLY=1] [EXTRA_QUEUES=n] [HIP_INIT=1] tools/aql/cp_latency mpich-pip_amd/lib/libmpir_hip_tiles.hsaco
+//   [HSA_ALLOCATE_QUEUE_DEV_MEM=1] [KARG_VRAM=1] [IDLE_ONLY=1] [EXTRA_QUEUES=n] [HIP_INIT=1] [NO_PROFILE=1] tools/aql/cp_latency mpich-pip_amd/lib/libmpir_hip_tiles.hsaco
 //
 // Cases (medians over 300 calls, us; all on the system timestamp clock):
 //   idle G      one dispatch, the host idles G us after the previous completion
@@ -221,7 +221,10 @@ int main(int argc, char **argv) {
     const hsa_queue_type32_t qtype = getenv("QUEUE_SINGLE") ? HSA_QUEUE_TYPE_SINGLE : HSA_QUEUE_TYPE_MULTI;
     printf("queue %s, %u packets\n", qtype == HSA_QUEUE_TYPE_SINGLE ? "single" : "multi", qsize);
     HK(hsa_queue_create(g_gpu, qsize, qtype, nullptr, nullptr, UINT32_MAX, UINT32_MAX, &g_q));
-    HK(hsa_amd_profiling_set_profiler_enabled(g_q, 1));
+    // NO_PROFILE=1: no CP timestamps (as the library's call queue runs); only
+    // the host-clock doorbell -> host sees interval is then meaningful
+    const bool prof = getenv("NO_PROFILE") == nullptr;
+    if (prof) HK(hsa_amd_profiling_set_profiler_enabled(g_q, 1));
     if (const char *pr = getenv("QUEUE_PRIORITY")) {
         const hsa_amd_queue_priority_t qp = !strcmp(pr, "high") ? HSA_AMD_QUEUE_PRIORITY_HIGH
                                            : !strcmp(pr, "low") ? HSA_AMD_QUEUE_PRIORITY_LOW
@@ -310,8 +313,8 @@ int main(int argc, char **argv) {
             hsa_signal_store_screlease(g_q->doorbell_signal, idx);
             wait(s1);
             const uint64_t t1 = ts();
-            uint64_t a, b;
-            times(s1, &a, &b);
+            uint64_t a = t0, b = t0;
+            if (prof) times(s1, &a, &b);
             if (k < 10) continue;
             d2s.push_back(us(a - t0));
             s2e.push_back(us(b - a));
