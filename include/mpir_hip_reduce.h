@@ -123,6 +123,10 @@ uint64_t MPIR_Hip_set_host_max_bytes(uint64_t bytes);
  * default 64 MiB.  The setter changes it at run time and returns the previous
  * value (bench.py reports config 2 both ways). */
 uint64_t MPIR_Hip_set_keep_bytes(uint64_t bytes);
+/* Results of at most `bytes` are stored nt whatever MPIR_Hip_set_keep_bytes says
+ * (MPIR_CVAR_REDUCE_LOCAL_KEEP_MIN_MB, default 16 MiB: below it sc1 costs the
+ * call more than its next reader gains); returns the previous value. */
+uint64_t MPIR_Hip_set_keep_min_bytes(uint64_t bytes);
 
 /* One operand host memory, the other on a device, at most this many bytes
  * (MPIR_CVAR_REDUCE_LOCAL_MIXED_MAX_KB, default 1 MiB): the host operand is

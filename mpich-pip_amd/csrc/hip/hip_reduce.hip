@@ -64,7 +64,22 @@ std::atomic<uint64_t> g_keep{[] {
 }()};
 uint64_t keep_bytes() { return g_keep.load(std::memory_order_relaxed); }
 
-uint64_t keep_for(uint64_t vbytes) { return vbytes <= keep_bytes() ? vbytes : 0; }
+// ... and results of at most this many bytes are stored nt again: below it the
+// sc1 stores cost the call more at the kernel's end than a next reader gains
+// from finding the result in the Infinity Cache (tools/keep_small_ab.py,
+// profiles/r06/keep_small_r06z.log: nt ahead by 0.3-1.0 us per call from 16 KiB
+// to 16 MiB whether or not the next call re-reads the result; sc1 ahead by
+// 0.6-1.7 us at 32-64 MiB when it does).  MPIR_CVAR_REDUCE_LOCAL_KEEP_MIN_MB,
+// default 16; MPIR_Hip_set_keep_min_bytes() at run time.
+std::atomic<uint64_t> g_keep_min{[] {
+    const char *e = getenv("MPIR_CVAR_REDUCE_LOCAL_KEEP_MIN_MB");
+    const long mb = e ? atol(e) : 16;
+    return (uint64_t)(mb >= 0 && mb <= 4096 ? mb : 16) << 20;
+}()};
+
+uint64_t keep_for(uint64_t vbytes) {
+    return vbytes > g_keep_min.load(std::memory_order_relaxed) && vbytes <= keep_bytes() ? vbytes : 0;
+}
 
 // MPIR_Hip_combine_set_flags: the calling thread's combine flags
 thread_local int t_combine_flags = 0;
@@ -1078,6 +1093,8 @@ uint64_t MPIR_Hip_host_max_bytes(void) { return host_max_bytes(); }
 uint64_t MPIR_Hip_set_host_max_bytes(uint64_t bytes) { return g_host_max.exchange(bytes); }
 
 uint64_t MPIR_Hip_set_keep_bytes(uint64_t bytes) { return mpir_hip::g_keep.exchange(bytes); }
+
+uint64_t MPIR_Hip_set_keep_min_bytes(uint64_t bytes) { return mpir_hip::g_keep_min.exchange(bytes); }
 
 uint64_t MPIR_Hip_mixed_max_bytes(void) { return mixed_max_bytes(); }
 

@@ -123,7 +123,8 @@ EXPORTED_SYMBOLS = [
     "MPIR_Hip_direct_last_kernel_ns", "MPIR_Hip_direct_state", "MPIR_Hip_direct_busy_skips",
     "MPIR_Hip_direct_last_split", "MPIR_Hip_direct_kernarg_writes", "MPIR_Hip_direct_placement", "MPIR_Hip_build_id", "MPIR_Hip_combine_set_flags",
     "MPIR_Hip_direct_prepare", "MPIR_Hip_set_local_ranks", "MPIR_Hip_host_threads",
-    "MPIR_Hip_default_rings_in_vram", "MPIR_Hip_direct_ring_location",
+    "MPIR_Hip_default_rings_in_vram", "MPIR_Hip_direct_ring_location", "MPIR_Hip_set_keep_bytes",
+    "MPIR_Hip_set_keep_min_bytes",
     # runtime subset for config 1 (include/mpi_pip.h)
     "MPI_Init", "MPI_Initialized", "MPI_Finalize", "MPI_Finalized", "MPI_Abort", "MPI_Comm_size",
     "MPI_Comm_rank", "MPI_Get_processor_name", "MPI_Wtime", "MPI_Wtick", "MPI_Barrier", "MPI_Bcast",
@@ -218,6 +219,9 @@ def load(path: str | None = None) -> ctypes.CDLL:
     lib.MPIR_Hip_default_rings_in_vram.restype = i32
     lib.MPIR_Hip_direct_ring_location.argtypes = [i32]
     lib.MPIR_Hip_direct_ring_location.restype = i32
+    for name in ("MPIR_Hip_set_keep_bytes", "MPIR_Hip_set_keep_min_bytes"):
+        getattr(lib, name).argtypes = [ctypes.c_uint64]
+        getattr(lib, name).restype = ctypes.c_uint64
     lib.MPIR_Hip_set_local_ranks.argtypes = [i32]
     lib.MPIR_Hip_set_local_ranks.restype = i32
     lib.MPIR_Hip_host_threads.argtypes = []
