@@ -381,7 +381,7 @@ static int group_exchange(struct MPIX_Hip_comm_s *c, const xfer_t *sends, int ns
  * pipelined folds keep their LDS cap: beside RCCL's kernel the capped fold
  * leaves it faster than the uncapped one (a one-rank all_reduce 56.9 against
  * 71.2 us, 21.8 alone), and in the pipeline the two are within
- * 1 % (tools/pipeline_overlap.cpp, profiles/r06/pipeline_overlap.log); a caller
+ * 1 % (tools/archive/pipeline_overlap.cpp, profiles/r06/pipeline_overlap.log); a caller
  * that wants the other choice has MPIR_Hip_combine_set_flags.
  * MPIR_CVAR_DEVICE_COLL_PIPELINE_KB: the chunk (default 32768 = 32 MiB; 0 =
  * never pipeline); a schedule pipelines when its largest block spans at least

@@ -1,19 +1,19 @@
 #!/usr/bin/env python3
 """How the synchronous call treats device buffers from each HIP allocator
-(round 6, after tools/pair_alloc_ab.py found hipDeviceMallocContiguous pairs
+(round 6, after tools/archive/pair_alloc_ab.py found hipDeviceMallocContiguous pairs
 ~2 us slower per call than hipMalloc ones, kernels alike): per method, one
 64 MiB fp32 pair; MPIR_Hip_pointer_kind of each operand, the share of 200
 calls the direct path took, the call median, and the profiled split (entry ->
 doorbell, doorbell -> CP start, kernel, CP end -> seen), medians, us.
 
-    python3 tools/alloc_kind_probe.py
+    python3 tools/archive/alloc_kind_probe.py
 """
 import ctypes
 import json
 import os
 import sys
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, os.path.join(ROOT, "mpich-pip_amd"))
 sys.path.insert(0, ROOT)
 

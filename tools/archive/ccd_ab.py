@@ -10,13 +10,13 @@ may use, rotating the order each round; per domain and round: the median of
 C loop, clock stamps per call.  Prints one JSON line per (round, domain), then
 per domain the median over rounds, its NUMA node and whether the GPU is there.
 
-    python3 tools/ccd_ab.py [rounds = 20]
+    python3 tools/archive/ccd_ab.py [rounds = 20]
 """
 import json
 import os
 import sys
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, os.path.join(ROOT, "mpich-pip_amd"))
 
 import mpich_pip_amd as m  # noqa: E402  (the library first: VRAM rings)

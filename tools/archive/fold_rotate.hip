@@ -16,8 +16,8 @@
 // + 6400 B for 96-192 MiB blocks), as the collectives lay them.
 //
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off \
-//         -Impich-pip_amd/csrc/hip -o tools/fold_rotate tools/fold_rotate.hip
-//   tools/fold_rotate [rounds = 9]
+//         -Impich-pip_amd/csrc/hip -o tools/archive/fold_rotate tools/archive/fold_rotate.hip
+//   tools/archive/fold_rotate [rounds = 9]
 #include <hip/hip_runtime.h>
 #include <algorithm>
 #include <cstdio>

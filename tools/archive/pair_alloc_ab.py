@@ -8,9 +8,9 @@ random tensors, and runs the headline call over them rotating (no call finds
 its operands in the Infinity Cache), C loop with clock stamps; per pair: the
 median call, and the median CP kernel time of profiled calls.
 
-    python3 tools/pair_alloc_ab.py METHOD [pairs = 12] [rounds = 40]
-    python3 tools/pair_alloc_ab.py --ab [reps = 3]     # alternates the methods in fresh processes
-    SHIFT=1 python3 tools/pair_alloc_ab.py contig       # + each pair with inbuf shifted by S bytes
+    python3 tools/archive/pair_alloc_ab.py METHOD [pairs = 12] [rounds = 40]
+    python3 tools/archive/pair_alloc_ab.py --ab [reps = 3]     # alternates the methods in fresh processes
+    SHIFT=1 python3 tools/archive/pair_alloc_ab.py contig       # + each pair with inbuf shifted by S bytes
 
 METHOD: torch (the bench's: one caching-allocator tensor per operand, with the
 bench's slack), malloc (hipMalloc per operand), contig (hipExtMallocWithFlags
@@ -23,7 +23,7 @@ import subprocess
 import sys
 import time
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, os.path.join(ROOT, "mpich-pip_amd"))
 sys.path.insert(0, ROOT)
 

@@ -6,14 +6,14 @@ transport), with the exchange pipelined against the fold
 alternated; wall time per collective call (all ranks), median over reps.  The
 results of the two are compared byte for byte.
 
-    python3 tools/pipeline_ab.py [reps = 7]
+    python3 tools/archive/pipeline_ab.py [reps = 7]
 """
 import os
 import sys
 import threading
 import time
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, os.path.join(ROOT, "mpich-pip_amd"))
 
 

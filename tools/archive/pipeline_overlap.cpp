@@ -3,9 +3,9 @@
 // fold running while chunk k+1's transfer runs, against the two one after the
 // other, with the fold's LDS cap on and off.
 //
-//   hipcc -O2 -std=c++17 -Iinclude -o tools/pipeline_overlap tools/pipeline_overlap.cpp \
+//   hipcc -O2 -std=c++17 -Iinclude -o tools/archive/pipeline_overlap tools/archive/pipeline_overlap.cpp \
 //         -Lmpich-pip_amd/lib -lmpir_hip -Wl,-rpath,$PWD/mpich-pip_amd/lib -lrccl
-//   tools/pipeline_overlap [reps = 15]
+//   tools/archive/pipeline_overlap [reps = 15]
 //
 // The transfer stand-in is RCCL's own kernel: a one-rank ncclAllReduce, fp16
 // SUM, over the (P - 1) chunks a rank receives in one group (7 x 32 MiB at

@@ -4,7 +4,7 @@ what the bracketing costs besides the calls -- the Python -> C loop entry and
 exit, and torch.cuda.synchronize() on an idle device -- and the raw profiled
 split of a few calls, bound near the GPU and unbound.
 
-    python3 tools/timing_overhead.py
+    python3 tools/archive/timing_overhead.py
 """
 import ctypes
 import json
@@ -12,7 +12,7 @@ import os
 import sys
 import time
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, os.path.join(ROOT, "mpich-pip_amd"))
 sys.path.insert(0, ROOT)
 

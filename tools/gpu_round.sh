@@ -21,14 +21,14 @@
 #   place2     the same with the waiting knobs (lazy / delay / flush polls) beside near and far
 #   place3     near / far callers with the completion signal on the GPU's node (sigg) or another (sigo)
 #   cpfloor    tools/aql/cp_floor.sh (the CP's doorbell -> start floor with HSA alone, then the product's split)
-#   ccd        tools/ccd_ab.py (the calling thread moved across L3 domains in one process)
-#   pairalloc  tools/pair_alloc_ab.py --ab (per-pair call and kernel medians under four allocation methods)
+#   ccd        tools/archive/ccd_ab.py (the calling thread moved across L3 domains in one process)
+#   pairalloc  tools/archive/pair_alloc_ab.py --ab (per-pair call and kernel medians under four allocation methods)
 #   pipe       the collectives' GPU tests (loopback, config sizes, fused schedules)
-#   overlap    tools/pipeline_overlap (fold beside a one-rank RCCL transfer, serial vs overlapped, capped or not)
-#   pipeab     tools/pipeline_ab.py (config 5 through the loopback, pipelined vs not)
-#   overhead   tools/timing_overhead.py (the timed region's bracketing cost; raw profiled splits), near and unbound
+#   overlap    tools/archive/pipeline_overlap (fold beside a one-rank RCCL transfer, serial vs overlapped, capped or not)
+#   pipeab     tools/archive/pipeline_ab.py (config 5 through the loopback, pipelined vs not)
+#   overhead   tools/archive/timing_overhead.py (the timed region's bracketing cost; raw profiled splits), near and unbound
 #   share2     BENCH_TEST_SHARE_GPU=1 bench.py --gpus 2 (the N > 1 path rehearsed on one GPU; not a measurement)
-#   rotate     tools/fold_rotate (P = 8 fold with rotated operand reads)
+#   rotate     tools/archive/fold_rotate (P = 8 fold with rotated operand reads)
 # Build every binary on the CPU side first (make -C mpich-pip_amd; hipcc lines
 # in each tool's header).
 set -o pipefail
@@ -81,21 +81,21 @@ PY
     place3) timeout -k 10 900 python -u tools/placement_ab.py 3 2000 near,near:sigg,near:sigo,far,far:sigg,far:sigo \
               > $OUT/placement_sig.log 2>&1; rc=$?; tail -9 $OUT/placement_sig.log ;;
     cpfloor) timeout -k 10 600 bash tools/aql/cp_floor.sh > $OUT/cp_floor.log 2>&1; rc=$?; grep -v '^{' $OUT/cp_floor.log | tail -30 ;;
-    ccd) timeout -k 10 300 python -u tools/ccd_ab.py 20 > $OUT/ccd_ab.log 2>&1; rc=$?; grep -v '^{"round' $OUT/ccd_ab.log | tail -24 ;;
-    pairalloc) timeout -k 10 600 python -u tools/pair_alloc_ab.py --ab 3 > $OUT/pair_alloc_ab.log 2>&1; rc=$?; tail -6 $OUT/pair_alloc_ab.log ;;
+    ccd) timeout -k 10 300 python -u tools/archive/ccd_ab.py 20 > $OUT/ccd_ab.log 2>&1; rc=$?; grep -v '^{"round' $OUT/ccd_ab.log | tail -24 ;;
+    pairalloc) timeout -k 10 600 python -u tools/archive/pair_alloc_ab.py --ab 3 > $OUT/pair_alloc_ab.log 2>&1; rc=$?; tail -6 $OUT/pair_alloc_ab.log ;;
     pipe) timeout -k 10 400 python -u -m pytest -x -q --timeout 200 --timeout-method thread \
                 tests/test_coll_loopback_gpu.py tests/test_config_size_gpu.py tests/test_schedule_fused_gpu.py \
                 > $OUT/pytest_pipe.log 2>&1; rc=$?; tail -2 $OUT/pytest_pipe.log ;;
-    overlap) timeout -k 10 200 tools/pipeline_overlap 15 > $OUT/pipeline_overlap.log 2>&1; rc=$?
+    overlap) timeout -k 10 200 tools/archive/pipeline_overlap 15 > $OUT/pipeline_overlap.log 2>&1; rc=$?
              cat $OUT/pipeline_overlap.log ;;
-    pipeab) timeout -k 10 300 python -u tools/pipeline_ab.py 7 > $OUT/pipeline_ab.log 2>&1; rc=$?
+    pipeab) timeout -k 10 300 python -u tools/archive/pipeline_ab.py 7 > $OUT/pipeline_ab.log 2>&1; rc=$?
             cat $OUT/pipeline_ab.log ;;
-    overhead) { timeout -k 10 120 python3 -u tools/timing_overhead.py > $OUT/overhead_near.log 2>&1 &&
-                timeout -k 10 120 python3 -u tools/timing_overhead.py unbound > $OUT/overhead_none.log 2>&1; }; rc=$?
+    overhead) { timeout -k 10 120 python3 -u tools/archive/timing_overhead.py > $OUT/overhead_near.log 2>&1 &&
+                timeout -k 10 120 python3 -u tools/archive/timing_overhead.py unbound > $OUT/overhead_none.log 2>&1; }; rc=$?
               cat $OUT/overhead_near.log $OUT/overhead_none.log ;;
     share2) BENCH_TEST_SHARE_GPU=1 timeout -k 10 300 python -u bench.py --gpus 2 --mib 64 --steps 10 --warmup 3 \
                 --collectives off > $OUT/bench_share2.log 2>&1; rc=$?; tail -c 1500 $OUT/bench_share2.log ;;
-    rotate) timeout -k 10 400 tools/fold_rotate 9 > $OUT/fold_rotate.log 2>&1; rc=$?; cat $OUT/fold_rotate.log ;;
+    rotate) timeout -k 10 400 tools/archive/fold_rotate 9 > $OUT/fold_rotate.log 2>&1; rc=$?; cat $OUT/fold_rotate.log ;;
     *) echo "unknown step $step"; rc=2 ;;
     esac
     if [ $rc -ne 0 ]; then echo "step $step failed: $rc"; exit $rc; fi
