@@ -1,4 +1,4 @@
-"""The committed bench line (profiles/r06/bench_r06t_ds.log, measured on MI355X) against
+"""The committed bench line (profiles/r06/bench_r06zc_ds.log, measured on MI355X) against
 the driver's contract and against itself: BASELINE.json's metric, the
 required keys, value = algorithmic bytes x N / time, roofline.frac =
 achieved / peak with achieved = 805,306,368 B / mean launch time, and the
@@ -10,7 +10,7 @@ import os
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LINE = os.path.join(ROOT, "profiles", "r06", "bench_r06t_ds.log")
+LINE = os.path.join(ROOT, "profiles", "r06", "bench_r06zc_ds.log")
 GIB = float(1 << 30)
 
 
